@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Benchmark: edges/sec to build the elimination tree (BASELINE.json metric), MI355X.
+
+One step = Sheep's timed window (graph2tree "Sorted" + "Mapped" [+ "Reduced"]) over one
+synthetic R-MAT graph already resident in HBM as u32 (tail, head) pairs:
+  degree histogram -> (degree, id) sort -> rank map -> edge pass -> tree build
+  [N > 1: RCCL degree all-reduce, per-GPU partial trees, log2(N) merge to rank 0].
+Workload: Graph500-style R-MAT scale 26, edgefactor 16 (1,073,741,824 records), seed 26 —
+the metric's config (BASELINE.json configs[3]); it fits one GPU, so N=1 runs it whole and
+N>1 shards the same records across ranks (strong scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu-baseline]
+N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md "HBM3E peak BW" (spec)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(scale, edgefactor, seed):
+    """Single-thread CPU restatement of graph2tree's Sorted+Mapped window (oracle, the
+    reference's algorithm with FastUnionFind) on a bounded sample: R-MAT `scale`."""
+    from oracle import oracle as O
+
+    uv = O.rmat(scale, edgefactor, seed)
+    sort_s, map_s, n_seq = O.time_graph2tree(uv, 1 << scale)
+    m = uv.shape[0]
+    return {"value": m / (sort_s + map_s), "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": "R-MAT scale %d ef%d seed %d (%d records, %d non-isolated), sort %.3fs + "
+                      "map %.3fs, CSR prebuilt (load excluded as in graph2tree), %s"
+                      % (scale, edgefactor, seed, m, n_seq, sort_s, map_s, cpu_model())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--edgefactor", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=26)
+    ap.add_argument("--cpu-scale", type=int, default=22)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify the tree against the CPU checker")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from sheep_amd import capi, device
+    from sheep_amd.dist import DeviceOps, build_tree_sharded, shard_bounds
+
+    device.init(local)
+    scale, ef, seed = args.scale, args.edgefactor, args.seed
+    m = ef << scale
+    n_ids = 1 << scale
+    lo, hi = shard_bounds(m, rank, world)
+    uv = device.rmat(scale, ef, seed, lo, hi)  # this rank's records, resident in HBM
+    torch.cuda.synchronize()
+    ops = DeviceOps()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def step():
+        if world == 1:
+            return device.graph2tree(uv, n_ids)
+        return build_tree_sharded(uv, n_ids, ops)
+
+    for _ in range(args.warmup):
+        out = step()
+    barrier()
+    phase = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+        for name, ms in capi.last_timings():
+            phase.setdefault(name, []).append(ms)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed / args.steps
+        n_seq = out[3] if world > 1 else out[3]
+        value = m / (elapsed / args.steps)
+        # Roofline of the dominant kernel (timed with HIP events on the library's stream, inside
+        # the timed steps).  Algorithmic bytes per launch are defined in DESIGN.md §Roofline.
+        avg = {k: sum(v) / len(v) for k, v in phase.items()}
+        algo = {
+            "tree_insert": 8 * m + 4 * n_seq,          # sorted (hi,lo) in, parent out
+            "bucket_sort": 2 * 2 * 8 * m,              # 2 radix passes x (read+write 8 B/rec)
+            "edge_pass": 8 * m + 8 * m + 4 * n_seq,    # records in, (hi,lo) out, pst
+            "sequence": 2 * 16 * n_ids,                # <=2 radix passes over (deg,id)
+            "degree": 8 * m + 4 * n_ids,               # records in, degree out
+        }
+        dom = max(avg, key=avg.get) if avg else None
+        roof = None
+        if dom:
+            ach = algo.get(dom, 0) / (avg[dom] * 1e-3)
+            roof = {"kernel": dom, "bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9,
+                    "unit": "GB/s", "frac": ach / HBM_PEAK, "traffic": None,
+                    "phases_ms": {k: round(v, 3) for k, v in avg.items()}}
+        path_bytes = 16 * m + 24 * n_seq  # SURVEY §8d B(m, n)
+        rec = {
+            "metric": "edges/sec to build elimination tree (RMAT-%d)" % scale,
+            "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic R-MAT (Graph500 A/B/C/D .57/.19/.19/.05), generated in HBM",
+            "config": {"workload": "rmat%d_ef%d" % (scale, ef), "scale": scale, "edgefactor": ef,
+                       "seed": seed, "records": m, "n_ids": n_ids, "n_seq": n_seq,
+                       "parallelism": "edge-shard x%d" % world if world > 1 else "single"},
+            "path_roofline": {"bytes": path_bytes,
+                              "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK)},
+            "roofline": roof,
+        }
+        if args.check:
+            rec["check"] = check_tree(out, scale, ef, seed)
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef, args.cpu_scale)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def check_tree(out, scale, ef, seed):
+    from oracle import oracle as O
+    import numpy as np
+
+    seq_d, parent_d, pst_d, n = out[0], out[1], out[2], out[3]
+    uv = O.rmat(scale, ef, seed)
+    seq = O.degree_sequence(uv)
+    p, s = O.build_tree(uv, seq)
+    ok = (n == len(seq)
+          and np.array_equal(seq_d[:n].cpu().numpy().view(np.uint32), seq)
+          and np.array_equal(parent_d[:n].cpu().numpy().view(np.uint32), p)
+          and np.array_equal(pst_d[:n].cpu().numpy().view(np.uint32), s))
+    return "bit-exact" if ok else "MISMATCH"
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/* sheep_amd.h — the C-ABI of the MI355X build of Sheep's tree-construction hot path.
+ *
+ * Drop-in boundary.  The reference has no FFI: its boundary is the header-only C++
+ * API in lib/ (sequence.h, jtree.h, jnode.h), consumed by the graph2tree / degree_sequence /
+ * merge_trees binaries.  Each entry point below replaces one reference interface; the C++
+ * host layer in sheep_amd/lib/ keeps the reference's C++ signatures and calls these.
+ *
+ * ABI rules:
+ *   - every call returns 0 (SHEEP_OK) or a negative errno-style code; no exception crosses the
+ *     ABI; sheep_last_error() gives the text of the calling thread's last failure;
+ *   - the caller owns every buffer; the library owns its device scratch (grown on demand,
+ *     released by sheep_release());
+ *   - host-pointer calls are synchronous; *_dev calls take device pointers and a HIP stream
+ *     (hipStream_t passed as void*, NULL = the library's stream) and return when the work is
+ *     ENQUEUED, except where a host-side count is returned (documented per call);
+ *   - calls are not re-entrant per device.
+ *
+ * Types follow lib/defs.h:76-82: ids, jnids and weights are uint32, INVALID = 0xFFFFFFFF.
+ * An edge stream is m records of (tail, head) as 2*m uint32 (the XS1 weight is dropped).
+ */
+#ifndef SHEEP_AMD_H
+#define SHEEP_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHEEP_OK 0
+#define SHEEP_INVALID 0xFFFFFFFFu
+
+/* Degree conventions.
+ * LLAMA: what graph2tree sees (graph_wrapper.h:87-89): a self-loop counts once.
+ * FILE:  degree_sequence's streaming count (sequence.h:101-107): a self-loop counts twice. */
+#define SHEEP_DEGREE_LLAMA 0
+#define SHEEP_DEGREE_FILE 1
+
+/* ---- device / library ------------------------------------------------------------------- */
+
+/* Select the HIP device for this thread's calls and create the library stream + scratch.
+ * Replaces the process/device setup around MPI_Init in graph2tree.cpp:134-157. */
+int sheep_gpu_init(int device);
+
+/* Free all device scratch held by the library on the current device. */
+int sheep_release(void);
+
+/* Text of the last error on this thread ("" if none). */
+const char* sheep_last_error(void);
+
+/* ABI version: (major << 16) | minor. */
+int sheep_abi_version(void);
+
+/* ---- host-pointer API (synchronous; what the reference's lib/ would bind) --------------- */
+
+/* Degree sequence: the ids with degree>0 ordered by (degree asc, id asc).
+ * Replaces degreeSequence (sequence.h:52-63) [LLAMA mode] and fileSequence_template
+ * (sequence.h:95-122) [FILE mode].  n_ids: every id in edges_uv must be < n_ids; pass 0 to
+ * take max id + 1.  seq_out must hold n_ids entries; *n_seq_out receives the length.
+ * rank_out (nullable, n_ids entries) receives jnid = position in seq, or INVALID. */
+int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                     uint32_t* seq_out, uint32_t* n_seq_out, uint32_t* rank_out);
+
+/* Elimination tree of the edge stream under seq: JNode{parent, pst_weight} per jnid.
+ * Replaces JTree(graph, seq[, file], Options()) (jtree.h:111-136 -> insertSequence
+ * jtree.cpp:112-145 -> insert jtree.cpp:65-110).  parent_out/pst_out hold n_seq entries.
+ * Errors: -EINVAL if seq repeats an id (the reference asserts, jtree.h:166);
+ *         -ERANGE if an edge joins a seq vertex to an id > max(seq) (index.at throws,
+ *         jtree.cpp:75). */
+int sheep_build_tree(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq, uint32_t n_seq,
+                     uint32_t* parent_out, uint32_t* pst_out);
+
+/* Associative tree union: etree(A ∪ B), pst summed (u32, wraps).
+ * Replaces JNodeTable::merge (jnode.cpp:174-201) as called by merge_trees.cpp:85-88 and by
+ * mpi_merge_reduction (jnode.cpp:203-211).  Both trees must come from the same seq. */
+int sheep_merge_trees(const uint32_t* parent_a, const uint32_t* pst_a, const uint32_t* parent_b,
+                      const uint32_t* pst_b, uint32_t n, uint32_t* parent_out, uint32_t* pst_out);
+
+/* ---- device-pointer API (the hot path; all pointers are device memory) ------------------ */
+
+/* deg[v] = degree of v over the m records (written, not accumulated); ids >= n_ids are an
+ * error (-ERANGE, reported by the next synchronising call).  Replaces the per-rank degree
+ * vector of mpiSequence (sequence.h:75-77). */
+int sheep_degree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                     uint32_t* d_deg, void* stream);
+
+/* seq/rank from a degree vector (after an all-reduce for sharded input: sequence.h:78-91).
+ * d_seq and d_rank hold n_ids entries.  Synchronises the stream; *n_seq_out is set. */
+int sheep_sequence_dev(const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq, uint32_t* d_rank,
+                       uint32_t* n_seq_out, void* stream);
+
+/* Partial or full elimination tree of the m records under the rank map d_rank (n_ids
+ * entries, INVALID for ids outside seq).  d_parent/d_pst hold n_seq entries.  Synchronises
+ * the stream (the tree builder sizes its passes on the host). */
+int sheep_build_tree_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_ids,
+                         uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst, void* stream);
+
+/* In-place merge: (parent_a, pst_a) <- etree(A ∪ B).  Enqueue only. */
+int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_t* d_parent_b,
+                          const uint32_t* d_pst_b, uint32_t n, void* stream);
+
+/* The whole single-device hot path: degree -> sequence -> tree (graph2tree's Sorted+Mapped).
+ * d_seq holds n_ids entries, d_parent/d_pst hold n_ids entries (n_seq used).  Synchronises. */
+int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                         uint32_t* d_seq, uint32_t* d_parent, uint32_t* d_pst,
+                         uint32_t* n_seq_out, void* stream);
+
+/* Synthetic R-MAT records [e_begin, e_end) of the stream (scale, seed) into d_uv
+ * (2*(e_end-e_begin) u32).  Bit-identical to sheep_amd/csrc/rmat.h on the host.  Enqueue only. */
+int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
+                   void* stream);
+
+/* Kernel timing of the last synchronising call (ms per named phase), for bench/profiling.
+ * Fills up to cap (name, ms) pairs; returns the count. */
+int sheep_last_timings(const char** names, double* ms, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHEEP_AMD_H */

@@ -1,0 +1,408 @@
+// The C-ABI (include/sheep_amd.h) over the HIP kernels in sheep_kernels.hip.
+//
+// Error model: every entry point catches everything, stores the text in a thread-local string
+// and returns a negative errno.  Device scratch is owned per device by a Ctx and grows on
+// demand; the hot path allocates nothing after its first call at a given size.
+#include <errno.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sheep_amd.h"
+#include "sheep_internal.h"
+
+namespace sheep {
+
+static thread_local std::string g_last_error;
+static thread_local int g_device = -1;
+static Ctx g_ctx[64];
+static std::mutex g_mu;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct ApiError : std::runtime_error {
+  int code;
+  ApiError(int c, const std::string& s) : std::runtime_error(s), code(c) {}
+};
+
+#define HIP_CHECK(x)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess)                                                                     \
+      throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));                         \
+  } while (0)
+
+void* Scratch::get(const char* name, size_t bytes) {
+  if (bytes == 0) bytes = 4;
+  for (auto& s : slots) {
+    if (s.first == name) {
+      if (s.second.bytes >= bytes) return s.second.p;
+      HIP_CHECK(hipFree(s.second.p));
+      s.second.p = nullptr;
+      s.second.bytes = 0;
+      HIP_CHECK(hipMalloc(&s.second.p, bytes));
+      s.second.bytes = bytes;
+      return s.second.p;
+    }
+  }
+  Slot sl;
+  HIP_CHECK(hipMalloc(&sl.p, bytes));
+  sl.bytes = bytes;
+  slots.emplace_back(name, sl);
+  return sl.p;
+}
+
+void Scratch::release() {
+  for (auto& s : slots)
+    if (s.second.p) (void)hipFree(s.second.p);
+  slots.clear();
+}
+
+static Ctx& init_ctx(int device) {
+  if (device < 0 || device >= 64) throw ApiError(-EINVAL, "device index out of range");
+  std::lock_guard<std::mutex> lk(g_mu);
+  Ctx& c = g_ctx[device];
+  HIP_CHECK(hipSetDevice(device));
+  if (c.device < 0) {
+    HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&c.d_err, 16));
+    HIP_CHECK(hipMemset(c.d_err, 0, 16));
+    HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
+    c.device = device;
+  }
+  g_device = device;
+  return c;
+}
+
+Ctx& ctx() {
+  if (g_device < 0) {
+    int d = 0;
+    HIP_CHECK(hipGetDevice(&d));
+    return init_ctx(d);
+  }
+  HIP_CHECK(hipSetDevice(g_device));
+  return g_ctx[g_device];
+}
+
+static hipStream_t pick(Ctx& c, void* stream) {
+  return stream ? (hipStream_t)stream : c.stream;
+}
+
+// Phase timing with HIP events on the working stream.
+struct Timer {
+  hipStream_t s;
+  std::vector<std::pair<const char*, hipEvent_t>> ev;
+  explicit Timer(hipStream_t st) : s(st) { mark("start"); }
+  void mark(const char* name) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, s));
+    ev.emplace_back(name, e);
+  }
+  void finish(Ctx& c) {  // after the stream has been synchronised
+    c.timings.clear();
+    for (size_t i = 1; i < ev.size(); ++i) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second);
+      c.timings.emplace_back(ev[i].first, (double)ms);
+    }
+  }
+  ~Timer() {
+    for (auto& e : ev) (void)hipEventDestroy(e.second);
+  }
+};
+
+// Read and clear the device error word (synchronises s).
+static void check_err(Ctx& c, hipStream_t s) {
+  HIP_CHECK(hipMemcpyAsync(c.h_pinned, c.d_err, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  uint32_t e = c.h_pinned[0];
+  if (e) {
+    HIP_CHECK(hipMemsetAsync(c.d_err, 0, 4, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (e & ERR_DUP_SEQ) throw ApiError(-EINVAL, "sequence repeats a vertex id");
+    if (e & ERR_RANGE) throw ApiError(-ERANGE, "vertex id out of range of the sequence/id space");
+  }
+}
+
+static inline int bits_for(uint64_t v) {  // number of significant bits
+  int b = 0;
+  while (v) { ++b; v >>= 1; }
+  return b;
+}
+
+// ---- device-level building blocks ---------------------------------------------------------
+
+static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
+                             uint32_t* d_rank, hipStream_t s) {
+  if (n_ids == 0) return 0;
+  uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
+  launch_deg_stats(d_deg, n_ids, stats, s);
+  HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  uint32_t maxdeg = c.h_pinned[0], zeros = c.h_pinned[1];
+  uint32_t n_seq = n_ids - zeros;
+  if (d_rank) launch_fill(d_rank, INV, n_ids, s);
+  if (n_seq == 0) return 0;
+  int passes = (bits_for(maxdeg) + 7) / 8;
+  uint32_t* ka = (uint32_t*)c.scratch.get("seq_ka", (size_t)n_ids * 4);
+  uint32_t* va = (uint32_t*)c.scratch.get("seq_va", (size_t)n_ids * 4);
+  uint32_t* kb = (uint32_t*)c.scratch.get("seq_kb", (size_t)n_ids * 4);
+  uint32_t* vb = (uint32_t*)c.scratch.get("seq_vb", (size_t)n_ids * 4);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("radix_tmp", radix_tmp_words(n_ids) * 4);
+  int which = radix_sort_pairs(d_deg, nullptr, ka, va, kb, vb, n_ids, 0, 8 * passes, tmp, s);
+  const uint32_t* sorted_ids = which == 0 ? va : vb;
+  HIP_CHECK(hipMemcpyAsync(d_seq, sorted_ids + zeros, (size_t)n_seq * 4, hipMemcpyDeviceToDevice, s));
+  if (d_rank) launch_rank_scatter(d_seq, n_seq, d_rank, c.d_err, s);
+  return n_seq;
+}
+
+static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
+                           uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
+                           hipStream_t s, Timer* tm) {
+  if (n_seq == 0) return;
+  launch_fill(d_parent, INV, n_seq, s);
+  launch_fill(d_pst, 0, n_seq, s);
+  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n_seq * 4);
+  launch_fill(jump, 0, n_seq, s);
+  if (m == 0) return;
+  uint32_t* hi = (uint32_t*)c.scratch.get("e_hi", m * 4);
+  uint32_t* lo = (uint32_t*)c.scratch.get("e_lo", m * 4);
+  uint32_t* ka = (uint32_t*)c.scratch.get("e_ka", m * 4);
+  uint32_t* va = (uint32_t*)c.scratch.get("e_va", m * 4);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("radix_tmp", radix_tmp_words(m) * 4);
+  launch_edge_pass(d_uv, m, d_rank, n_rank, d_pst, hi, lo, c.d_err, s);
+  if (tm) tm->mark("edge_pass");
+  // Bucket the tree edges by the top 16 bits of hi (approximate Liu order; exactness does not
+  // depend on the order, only the amount of zipper work does).
+  int top = bits_for(n_seq);
+  int lo_bit = std::max(0, top - 16);
+  int which = radix_sort_pairs(hi, lo, ka, va, hi, lo, m, lo_bit, top, tmp, s);
+  const uint32_t* shi = which == 0 ? ka : hi;
+  const uint32_t* slo = which == 0 ? va : lo;
+  if (tm) tm->mark("bucket_sort");
+  launch_tree_insert(shi, slo, m, d_parent, jump, s);
+  if (tm) tm->mark("tree_insert");
+}
+
+}  // namespace sheep
+
+using namespace sheep;
+
+#define API_BEGIN try {
+#define API_END                                                                               \
+  }                                                                                           \
+  catch (const ApiError& e) {                                                                 \
+    g_last_error = e.what();                                                                  \
+    return e.code;                                                                            \
+  }                                                                                           \
+  catch (const HipError& e) {                                                                 \
+    g_last_error = e.what();                                                                  \
+    return -EIO;                                                                              \
+  }                                                                                           \
+  catch (const std::bad_alloc&) {                                                             \
+    g_last_error = "out of memory";                                                           \
+    return -ENOMEM;                                                                           \
+  }                                                                                           \
+  catch (const std::exception& e) {                                                           \
+    g_last_error = e.what();                                                                  \
+    return -EIO;                                                                              \
+  }                                                                                           \
+  return SHEEP_OK;
+
+static void require_aligned(const void* p, const char* what) {
+  if (((uintptr_t)p) & 7u) throw ApiError(-EINVAL, std::string(what) + " must be 8-byte aligned");
+}
+
+extern "C" {
+
+int sheep_abi_version(void) { return (1 << 16) | 0; }
+
+const char* sheep_last_error(void) { return g_last_error.c_str(); }
+
+int sheep_gpu_init(int device) {
+  API_BEGIN
+  init_ctx(device);
+  g_last_error.clear();
+  API_END
+}
+
+int sheep_release(void) {
+  API_BEGIN
+  Ctx& c = ctx();
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.scratch.release();
+  API_END
+}
+
+int sheep_last_timings(const char** names, double* ms, int cap) {
+  Ctx& c = g_ctx[g_device < 0 ? 0 : g_device];
+  int n = std::min<int>(cap, (int)c.timings.size());
+  for (int i = 0; i < n; ++i) {
+    names[i] = c.timings[i].first;
+    ms[i] = c.timings[i].second;
+  }
+  return n;
+}
+
+// ---- device-pointer API -------------------------------------------------------------------
+
+int sheep_degree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                     uint32_t* d_deg, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  launch_degree(d_uv, m, n_ids, degree_mode, d_deg, c.d_err, pick(c, stream));
+  API_END
+}
+
+int sheep_sequence_dev(const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq, uint32_t* d_rank,
+                       uint32_t* n_seq_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = pick(c, stream);
+  uint32_t n = sequence_dev(c, d_deg, n_ids, d_seq, d_rank, s);
+  check_err(c, s);
+  if (n_seq_out) *n_seq_out = n;
+  API_END
+}
+
+int sheep_build_tree_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_rank,
+                         uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  hipStream_t s = pick(c, stream);
+  Timer tm(s);
+  build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, &tm);
+  check_err(c, s);
+  tm.finish(c);
+  API_END
+}
+
+int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_t* d_parent_b,
+                          const uint32_t* d_pst_b, uint32_t n, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = pick(c, stream);
+  uint32_t* jump = (uint32_t*)c.scratch.get("merge_jump", (size_t)n * 4);
+  launch_merge(d_parent_a, d_pst_a, d_parent_b, d_pst_b, n, jump, s);
+  API_END
+}
+
+int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                         uint32_t* d_seq, uint32_t* d_parent, uint32_t* d_pst,
+                         uint32_t* n_seq_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  hipStream_t s = pick(c, stream);
+  Timer tm(s);
+  uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
+  launch_degree(d_uv, m, n_ids, degree_mode, deg, c.d_err, s);
+  tm.mark("degree");
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
+  tm.mark("sequence");
+  build_tree_dev(c, d_uv, m, rank, n_ids, n_seq, d_parent, d_pst, s, &tm);
+  check_err(c, s);
+  tm.finish(c);
+  if (n_seq_out) *n_seq_out = n_seq;
+  API_END
+}
+
+int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
+                   void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (scale < 1 || scale > 32) throw ApiError(-EINVAL, "scale must be in [1, 32]");
+  launch_rmat(d_uv, scale, seed, e_begin, e_end, pick(c, stream));
+  API_END
+}
+
+// ---- host-pointer API ----------------------------------------------------------------------
+
+int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                     uint32_t* seq_out, uint32_t* n_seq_out, uint32_t* rank_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = c.stream;
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  if (n_ids == 0)
+    for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", 8 * m);
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
+  uint32_t* seq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_ids * 4);
+  launch_degree(uv, m, n_ids, degree_mode, deg, c.d_err, s);
+  check_err(c, s);
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, seq, rank, s);
+  if (n_seq) HIP_CHECK(hipMemcpyAsync(seq_out, seq, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  if (rank_out && n_ids)
+    HIP_CHECK(hipMemcpyAsync(rank_out, rank, (size_t)n_ids * 4, hipMemcpyDeviceToHost, s));
+  check_err(c, s);
+  if (n_seq_out) *n_seq_out = n_seq;
+  API_END
+}
+
+int sheep_build_tree(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq, uint32_t n_seq,
+                     uint32_t* parent_out, uint32_t* pst_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = c.stream;
+  if (n_seq == 0) return SHEEP_OK;
+  uint32_t n_rank = *std::max_element(seq, seq + n_seq) + 1;  // reference index size, jtree.h:113
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", 8 * m);
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_seq * 4);
+  HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_rank * 4);
+  launch_fill(rank, INV, n_rank, s);
+  launch_rank_scatter(dseq, n_seq, rank, c.d_err, s);
+  check_err(c, s);
+  uint32_t* parent = (uint32_t*)c.scratch.get("h_parent", (size_t)n_seq * 4);
+  uint32_t* pst = (uint32_t*)c.scratch.get("h_pst", (size_t)n_seq * 4);
+  Timer tm(s);
+  build_tree_dev(c, uv, m, rank, n_rank, n_seq, parent, pst, s, &tm);
+  check_err(c, s);
+  tm.finish(c);
+  HIP_CHECK(hipMemcpyAsync(parent_out, parent, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(pst_out, pst, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  API_END
+}
+
+int sheep_merge_trees(const uint32_t* parent_a, const uint32_t* pst_a, const uint32_t* parent_b,
+                      const uint32_t* pst_b, uint32_t n, uint32_t* parent_out, uint32_t* pst_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = c.stream;
+  if (n == 0) return SHEEP_OK;
+  size_t b = (size_t)n * 4;
+  uint32_t* pa = (uint32_t*)c.scratch.get("m_pa", b);
+  uint32_t* sa = (uint32_t*)c.scratch.get("m_sa", b);
+  uint32_t* pb = (uint32_t*)c.scratch.get("m_pb", b);
+  uint32_t* sb = (uint32_t*)c.scratch.get("m_sb", b);
+  HIP_CHECK(hipMemcpyAsync(pa, parent_a, b, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(sa, pst_a, b, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(pb, parent_b, b, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(sb, pst_b, b, hipMemcpyHostToDevice, s));
+  uint32_t* jump = (uint32_t*)c.scratch.get("merge_jump", b);
+  launch_merge(pa, sa, pb, sb, n, jump, s);
+  HIP_CHECK(hipMemcpyAsync(parent_out, pa, b, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(pst_out, sa, b, hipMemcpyDeviceToHost, s));
+  check_err(c, s);
+  API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// Internal declarations shared by the HIP kernels (sheep_kernels.hip) and the C-ABI
+// (sheep_capi.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace sheep {
+
+constexpr uint32_t INV = 0xFFFFFFFFu;
+
+// Bits of the device error word (OR-ed by kernels, read by the host after a sync).
+constexpr uint32_t ERR_RANGE = 1u;      // an id >= n_ids, or index.at(nbr) out of range
+constexpr uint32_t ERR_DUP_SEQ = 2u;    // an id repeated in seq
+
+// Growable device scratch.  One instance per device; slots are named so that the hot path
+// reuses its buffers across calls (allocation only happens on the first / a larger call).
+struct Scratch {
+  struct Slot { void* p = nullptr; size_t bytes = 0; };
+  std::vector<std::pair<std::string, Slot>> slots;
+  void* get(const char* name, size_t bytes);  // throws std::runtime_error on hipMalloc failure
+  void release();
+};
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  Scratch scratch;
+  uint32_t* d_err = nullptr;     // device error word
+  uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
+  std::vector<std::pair<const char*, double>> timings;
+};
+
+Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)
+
+// ---- launchers (sheep_kernels.hip); all enqueue on `s` -------------------------------------
+void launch_degree(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
+                   uint32_t* err, hipStream_t s);
+void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max,[1]=zeros*/,
+                      hipStream_t s);
+// Exclusive scan of n u32 (n < 2^32); tmp needs scan_tmp_words(n) u32.
+size_t scan_tmp_words(uint64_t n);
+void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp,
+                           hipStream_t s);
+// Stable LSD radix sort of (key, val) pairs on bits [bit_lo, bit_hi) of key.  vals_in NULL
+// means val = index.  Buffers a/b ping-pong; returns which buffer (0 = a, 1 = b) holds the
+// result.  tmp needs radix_tmp_words(n) u32.
+size_t radix_tmp_words(uint64_t n);
+int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_a,
+                     uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, uint64_t n, int bit_lo,
+                     int bit_hi, uint32_t* tmp, hipStream_t s);
+void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s);
+void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
+                         hipStream_t s);
+void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                      uint32_t* pst, uint32_t* hi_out, uint32_t* lo_out, uint32_t* err,
+                      hipStream_t s);
+void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
+                        uint32_t* jump, hipStream_t s);
+void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
+                  const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
+void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
+                 hipStream_t s);
+
+}  // namespace sheep

@@ -1,0 +1,457 @@
+// HIP kernels for gfx950 (MI355X) — Sheep's tree-construction hot path.
+//
+// All arithmetic is u32 integer work bound by HBM traffic, random gathers and atomics; nothing
+// here is GEMM-shaped, so there is no MFMA.  Wave = 64 lanes throughout (ballots are 64-bit).
+//
+//   k_degree        per-vertex degree (sequence.h:101-107 / graph_wrapper.h:87-89)
+//   k_radix_*       stable LSD radix sort, LDS-ranked per 4096-key tile (degree sequence:
+//                   sequence.h:55-61; edge bucketing by max(rank))
+//   k_scan_*        exclusive scan (radix offsets)
+//   k_edge_pass     rank translation, pst_weight (jtree.cpp:84-87), (lo,hi) tree edges
+//   k_tree_insert   lock-free elimination-tree insertion ("zipper"), replacing the
+//                   union-find loop jtree.cpp:73-83 + unionfind.h:46-102
+//   k_merge         associative tree union (jnode.cpp:174-201) with the same insertion
+//   k_rmat          synthetic input generator (rmat.h)
+#include <hip/hip_runtime.h>
+
+#include "rmat.h"
+#include "sheep_internal.h"
+
+namespace sheep {
+
+static constexpr int BLOCK = 256;
+static constexpr int ITEMS = 16;
+static constexpr int TILE = BLOCK * ITEMS;  // keys per radix/scan tile
+static constexpr int MAX_GRID = 256 * 8;    // 8 blocks of 256 per CU over 256 CUs
+
+static inline unsigned grid_for(uint64_t n, int per_block = BLOCK) {
+  uint64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > MAX_GRID) g = MAX_GRID;
+  return (unsigned)g;
+}
+
+// ---------------------------------------------------------------------------------------
+// Degree.  LLAMA mode: deg[t]++, deg[h]++ unless t == h (a self-loop is one adjacency entry,
+// graph_wrapper.h:43-63 as loaded LL_L_UNDIRECTED_DOUBLE).  FILE mode: deg[t]++, deg[h]++
+// always (sequence.h:105-106).
+// ---------------------------------------------------------------------------------------
+__global__ void k_degree(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode,
+                         uint32_t* __restrict__ deg, uint32_t* err) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    uint2 e = uv[i];
+    if (e.x >= n_ids || e.y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
+    atomicAdd(&deg[e.x], 1u);
+    if (file_mode || e.x != e.y) atomicAdd(&deg[e.y], 1u);
+  }
+}
+
+void launch_degree(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
+                   uint32_t* err, hipStream_t s) {
+  if (n_ids) (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
+  if (m == 0) return;
+  hipLaunchKernelGGL(k_degree, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, n_ids,
+                     file_mode, deg, err);
+}
+
+// stats[0] = max degree, stats[1] = number of zero-degree ids.
+__global__ void k_deg_stats(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* stats) {
+  uint32_t mx = 0, zeros = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t d = deg[i];
+    mx = max(mx, d);
+    zeros += (d == 0);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    zeros += (uint32_t)__shfl_xor((int)zeros, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&stats[0], mx);
+    atomicAdd(&stats[1], zeros);
+  }
+}
+
+void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats, hipStream_t s) {
+  (void)hipMemsetAsync(stats, 0, 8, s);
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_deg_stats, dim3(grid_for(n)), dim3(BLOCK), 0, s, deg, n, stats);
+}
+
+__global__ void k_fill(uint32_t* p, uint32_t v, uint64_t n) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s) {
+  if (n == 0) return;
+  if (value == 0 || value == INV) {
+    (void)hipMemsetAsync(p, value ? 0xFF : 0, n * 4, s);
+    return;
+  }
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(BLOCK), 0, s, p, value, n);
+}
+
+// ---------------------------------------------------------------------------------------
+// Exclusive scan (u32), TILE elements per block: reduce -> scan of block sums -> downsweep.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = (uint32_t)__shfl_up((int)v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan of one TILE held in LDS (tile[0..TILE)); returns the tile total.
+__device__ uint32_t block_scan_tile(uint32_t* tile, uint32_t* wsum) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t local[ITEMS];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) { local[i] = tile[t * ITEMS + i]; sum += local[i]; }
+  uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < BLOCK / 64; ++i) { if (i < w) wbase += wsum[i]; total += wsum[i]; }
+  uint32_t run = wbase + incl - sum;
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) { tile[t * ITEMS + i] = run; run += local[i]; }
+  __syncthreads();
+  return total;
+}
+
+__global__ void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n, uint32_t* sums) {
+  uint64_t base = (uint64_t)blockIdx.x * TILE;
+  uint32_t s = 0;
+  for (int i = 0; i < ITEMS; ++i) {
+    uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
+    if (idx < n) s += in[idx];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
+  __shared__ uint32_t ws[BLOCK / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < BLOCK / 64; ++i) t += ws[i];
+    sums[blockIdx.x] = t;
+  }
+}
+
+__global__ void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                            uint64_t n, const uint32_t* __restrict__ offsets) {
+  __shared__ uint32_t tile[TILE];
+  __shared__ uint32_t wsum[BLOCK / 64];
+  uint64_t base = (uint64_t)blockIdx.x * TILE;
+  for (int i = 0; i < ITEMS; ++i) {
+    uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
+    tile[i * BLOCK + threadIdx.x] = idx < n ? in[idx] : 0;
+  }
+  __syncthreads();
+  block_scan_tile(tile, wsum);
+  uint32_t off = offsets ? offsets[blockIdx.x] : 0;
+  for (int i = 0; i < ITEMS; ++i) {
+    uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
+    if (idx < n) out[idx] = tile[i * BLOCK + threadIdx.x] + off;
+  }
+}
+
+size_t scan_tmp_words(uint64_t n) {
+  size_t words = 0;
+  while (n > (uint64_t)TILE) {
+    n = (n + TILE - 1) / TILE;
+    words += n;
+  }
+  return words + 1;
+}
+
+void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp,
+                           hipStream_t s) {
+  if (n == 0) return;
+  if (n <= (uint64_t)TILE) {
+    hipLaunchKernelGGL(k_scan_down, dim3(1), dim3(BLOCK), 0, s, in, out, n, (const uint32_t*)nullptr);
+    return;
+  }
+  uint64_t nb = (n + TILE - 1) / TILE;
+  uint32_t* sums = tmp;
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(BLOCK), 0, s, in, n, sums);
+  launch_scan_exclusive(sums, sums, nb, tmp + nb, s);  // in-place: each tile is read before written
+  hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(BLOCK), 0, s, in, out, n,
+                     (const uint32_t*)sums);
+}
+
+// ---------------------------------------------------------------------------------------
+// Stable LSD radix sort, 8-bit digits.  Pass = count (LDS histogram per tile, digit-major
+// counts matrix) -> exclusive scan -> scatter (per-chunk stable ranking by 64-lane ballot
+// match + per-wave digit counts in LDS).
+// ---------------------------------------------------------------------------------------
+__global__ void k_radix_count(const uint32_t* __restrict__ keys, uint64_t n, int shift,
+                              uint32_t* __restrict__ counts, uint32_t nblocks) {
+  __shared__ uint32_t hist[256];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t base = (uint64_t)blockIdx.x * TILE;
+  for (int i = 0; i < ITEMS; ++i) {
+    uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
+    if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  counts[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = hist[threadIdx.x];
+}
+
+__global__ void k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                const uint32_t* __restrict__ vals_in,
+                                uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                uint64_t n, int shift, const uint32_t* __restrict__ offsets,
+                                uint32_t nblocks) {
+  __shared__ uint32_t running[256];
+  __shared__ uint32_t whist[BLOCK / 64][256];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  running[t] = offsets[(uint64_t)t * nblocks + blockIdx.x];
+  for (int i = 0; i < BLOCK / 64; ++i) whist[i][t] = 0;
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint64_t base = (uint64_t)blockIdx.x * TILE;
+  for (int c = 0; c < ITEMS; ++c) {
+    uint64_t idx = base + (uint64_t)c * BLOCK + t;
+    bool valid = idx < n;
+    uint32_t key = valid ? keys_in[idx] : 0u;
+    uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    uint32_t d = (key >> shift) & 255u;
+    uint64_t match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      bool bit = (d >> b) & 1u;
+      uint64_t bal = __ballot(bit);
+      match &= bit ? bal : ~bal;
+    }
+    uint32_t before = (uint32_t)__popcll(match & lt);
+    if (valid && before == 0) whist[w][d] = (uint32_t)__popcll(match);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = running[d] + before;
+      for (int i = 0; i < w; ++i) pos += whist[i][d];
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    for (int i = 0; i < BLOCK / 64; ++i) { tot += whist[i][t]; whist[i][t] = 0; }
+    running[t] += tot;
+    __syncthreads();
+  }
+}
+
+size_t radix_tmp_words(uint64_t n) {
+  uint64_t nb = (n + TILE - 1) / TILE;
+  return 256 * nb + scan_tmp_words(256 * nb);
+}
+
+int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_a,
+                     uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, uint64_t n, int bit_lo,
+                     int bit_hi, uint32_t* tmp, hipStream_t s) {
+  uint64_t nb = (n + TILE - 1) / TILE;
+  uint32_t* counts = tmp;
+  uint32_t* stmp = tmp + 256 * nb;
+  const uint32_t* kin = keys_in;
+  const uint32_t* vin = vals_in;
+  int cur = -1;
+  for (int shift = bit_lo; shift < bit_hi; shift += 8) {
+    uint32_t* kout = (cur == 0) ? keys_b : keys_a;
+    uint32_t* vout = (cur == 0) ? vals_b : vals_a;
+    if (n) {
+      hipLaunchKernelGGL(k_radix_count, dim3((unsigned)nb), dim3(BLOCK), 0, s, kin, n, shift,
+                         counts, (uint32_t)nb);
+      launch_scan_exclusive(counts, counts, 256 * nb, stmp, s);
+      hipLaunchKernelGGL(k_radix_scatter, dim3((unsigned)nb), dim3(BLOCK), 0, s, kin, vin, kout,
+                         vout, n, shift, (const uint32_t*)counts, (uint32_t)nb);
+    }
+    cur = (cur == 0) ? 1 : 0;
+    kin = kout;
+    vin = vout;
+  }
+  return cur;
+}
+
+// ---------------------------------------------------------------------------------------
+// rank[seq[i]] = i (JTree::insert(X, id), jtree.h:165-168).  A repeated id trips the
+// reference's assert; here it sets ERR_DUP_SEQ.
+// ---------------------------------------------------------------------------------------
+__global__ void k_rank_scatter(const uint32_t* __restrict__ seq, uint32_t n_seq,
+                               uint32_t* __restrict__ rank, uint32_t* err) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_seq; i += gridDim.x * blockDim.x) {
+    if (atomicCAS(&rank[seq[i]], INV, i) != INV) atomicOr(err, ERR_DUP_SEQ);
+  }
+}
+
+void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
+                         hipStream_t s) {
+  if (n_seq == 0) return;
+  hipLaunchKernelGGL(k_rank_scatter, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, seq, n_seq, rank, err);
+}
+
+// ---------------------------------------------------------------------------------------
+// Edge pass (JTree::insert's edge loop, jtree.cpp:73-90, edge-parallel): for record (t,h),
+// t != h, in jnid space lo = min(rank), hi = max(rank) with INVALID = +inf:
+//   lo valid           -> pst_weight[lo] += 1        (the POSTORDER edge seen from lo)
+//   lo, hi both valid  -> tree edge (lo, hi)         (the PREORDER edge seen from hi)
+// Ids >= n_rank are outside the reference's index vector: if the other endpoint is in seq the
+// reference's index.at() throws (jtree.cpp:75) -> ERR_RANGE; otherwise neither endpoint is
+// ever visited and the record is ignored.
+// ---------------------------------------------------------------------------------------
+__global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
+                            const uint32_t* __restrict__ rank, uint32_t n_rank,
+                            uint32_t* __restrict__ pst, uint32_t* __restrict__ hi_out,
+                            uint32_t* __restrict__ lo_out, uint32_t* err) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    uint2 e = uv[i];
+    uint32_t hi = INV, lo = INV;
+    if (e.x != e.y) {
+      bool ox = e.x >= n_rank, oy = e.y >= n_rank;
+      uint32_t rx = ox ? INV : rank[e.x];
+      uint32_t ry = oy ? INV : rank[e.y];
+      if ((ox && ry != INV) || (oy && rx != INV)) {
+        atomicOr(err, ERR_RANGE);
+      } else {
+        lo = min(rx, ry);
+        hi = max(rx, ry);
+        if (lo != INV) atomicAdd(&pst[lo], 1u);
+      }
+    }
+    hi_out[i] = hi;
+    lo_out[i] = lo;
+  }
+}
+
+void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                      uint32_t* pst, uint32_t* hi_out, uint32_t* lo_out, uint32_t* err,
+                      hipStream_t s) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(k_edge_pass, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, rank,
+                     n_rank, pst, hi_out, lo_out, err);
+}
+
+// ---------------------------------------------------------------------------------------
+// Lock-free elimination-tree insertion.
+//
+// State: parent[] is a heap-ordered forest (parent > child, INVALID = root) and a set of
+// pending edges.  Invariant: etree(parent-forest ∪ pending) = etree(all edges inserted so
+// far).  Inserting pending edge (a, b), a < b:
+//   walk up from a to a vertex x < b whose parent p is >= b (or INVALID);
+//     p == b       -> a already hangs below b: drop the edge;
+//     p == INVALID -> CAS parent[x]: INVALID -> b, done;
+//     p >  b       -> CAS parent[x]: p -> b, then insert pending (b, p)  ("zipper" step).
+// Each step is one CAS on one word and preserves the threshold-connectivity of the graph at
+// every rank, hence the etree (SURVEY §7 "Hard parts" fact 3).  A failed CAS returns the
+// current value and the walk resumes from it.  parent values only ever decrease, so a stale
+// (L2-cached) read is always a former ancestor: walking to it is still valid, and CASing on it
+// fails and refreshes.  jump[] is a hint array of former ancestors (path splitting) that only
+// accelerates the walk.  When no edge is pending the forest is the etree of every inserted
+// edge — the same unique result as Liu's sequential union-find (jtree.cpp:73-83,
+// unionfind.h:46-102), independent of insertion order and interleaving.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_parent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void zip_insert(uint32_t* __restrict__ parent, uint32_t* __restrict__ jump, uint32_t a,
+                           uint32_t b) {
+  uint32_t x = a, prev = INV, p = 0;
+  bool fresh = false;
+  for (;;) {
+    if (!fresh) {
+      uint32_t j = jump[x];
+      if (j > x && j < b) {
+        if (prev != INV) jump[prev] = j;
+        prev = x;
+        x = j;
+        continue;
+      }
+      p = ld_parent(&parent[x]);
+    }
+    fresh = false;
+    if (p < b) {  // INVALID is never < b
+      if (prev != INV) jump[prev] = p;
+      prev = x;
+      x = p;
+      continue;
+    }
+    if (x != a) jump[a] = x;
+    if (p == b) return;
+    uint32_t old = atomicCAS(&parent[x], p, b);
+    if (old != p) {
+      p = old;
+      fresh = true;
+      continue;
+    }
+    if (p == INV) return;
+    a = b;
+    b = p;
+    x = a;
+    prev = INV;
+  }
+}
+
+__global__ void k_tree_insert(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                              uint64_t n, uint32_t* parent, uint32_t* jump) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t b = hi[i];
+    if (b == INV) continue;
+    zip_insert(parent, jump, lo[i], b);
+  }
+}
+
+void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
+                        uint32_t* jump, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_tree_insert, dim3(grid_for(n)), dim3(BLOCK), 0, s, hi, lo, n, parent, jump);
+}
+
+// Merge (jnode.cpp:174-201): insert every edge (v, parent_b[v]) of tree B into tree A;
+// pst_weight sums (u32 wrap-around, as the reference's esize_t += ).
+__global__ void k_merge(uint32_t* parent_a, uint32_t* __restrict__ pst_a,
+                        const uint32_t* __restrict__ parent_b, const uint32_t* __restrict__ pst_b,
+                        uint32_t n, uint32_t* jump) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+    pst_a[v] += pst_b[v];
+    uint32_t p = parent_b[v];
+    if (p != INV) zip_insert(parent_a, jump, v, p);
+  }
+}
+
+void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
+                  const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s) {
+  if (n == 0) return;
+  (void)hipMemsetAsync(jump, 0, (size_t)n * 4, s);
+  hipLaunchKernelGGL(k_merge, dim3(grid_for(n)), dim3(BLOCK), 0, s, parent_a, pst_a, parent_b,
+                     pst_b, n, jump);
+}
+
+// ---------------------------------------------------------------------------------------
+// R-MAT generator (rmat.h).
+// ---------------------------------------------------------------------------------------
+__global__ void k_rmat(uint2* __restrict__ uv, int scale, uint64_t seed, uint64_t e_begin,
+                       uint64_t n) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t t, h;
+    sheep_rmat::edge(e_begin + i, scale, seed, &t, &h);
+    uv[i] = make_uint2(t, h);
+  }
+}
+
+void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
+                 hipStream_t s) {
+  if (e_end <= e_begin) return;
+  hipLaunchKernelGGL(k_rmat, dim3(grid_for(e_end - e_begin)), dim3(BLOCK), 0, s, (uint2*)uv, scale,
+                     seed, e_begin, e_end - e_begin);
+}
+
+}  // namespace sheep

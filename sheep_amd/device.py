@@ -1,0 +1,75 @@
+"""Device-resident hot path: torch owns HBM buffers and streams, libsheep_amd.so does the work.
+
+Every function takes torch tensors on a ``cuda`` (HIP) device and enqueues on torch's current
+stream, so it composes with torch.distributed (RCCL) collectives on the same stream.
+"""
+import ctypes
+
+import torch
+
+from . import capi
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def init(device_index):
+    capi.call("sheep_gpu_init", int(device_index))
+
+
+def rmat(scale, edgefactor, seed, e_begin=0, e_end=None, device="cuda"):
+    """R-MAT records [e_begin, e_end) of the (scale, seed) stream as an (n, 2) uint32 tensor."""
+    m = edgefactor << scale
+    if e_end is None:
+        e_end = m
+    uv = torch.empty((e_end - e_begin, 2), dtype=torch.uint32, device=device)
+    capi.call("sheep_rmat_dev", _p(uv), scale, seed, e_begin, e_end, _stream())
+    return uv
+
+
+def degree(uv, n_ids, mode=capi.DEGREE_LLAMA, out=None):
+    deg = out if out is not None else torch.empty(n_ids, dtype=torch.uint32, device=uv.device)
+    capi.call("sheep_degree_dev", _p(uv), uv.shape[0], n_ids, mode, _p(deg), _stream())
+    return deg
+
+
+def sequence(deg, seq=None, rank=None):
+    n_ids = deg.numel()
+    seq = seq if seq is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=deg.device)
+    rank = rank if rank is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32,
+                                                     device=deg.device)
+    n_seq = ctypes.c_uint32(0)
+    capi.call("sheep_sequence_dev", _p(deg), n_ids, _p(seq), _p(rank), ctypes.byref(n_seq),
+              _stream())
+    return seq, rank, n_seq.value
+
+
+def build_tree(uv, rank, n_seq, parent=None, pst=None):
+    parent = parent if parent is not None else torch.empty(max(n_seq, 1), dtype=torch.uint32,
+                                                           device=uv.device)
+    pst = pst if pst is not None else torch.empty(max(n_seq, 1), dtype=torch.uint32, device=uv.device)
+    capi.call("sheep_build_tree_dev", _p(uv), uv.shape[0], _p(rank), rank.numel(), n_seq,
+              _p(parent), _p(pst), _stream())
+    return parent, pst
+
+
+def merge_into(parent_a, pst_a, parent_b, pst_b, n):
+    """(parent_a, pst_a) <- etree(A ∪ B), in place."""
+    capi.call("sheep_merge_trees_dev", _p(parent_a), _p(pst_a), _p(parent_b), _p(pst_b), n,
+              _stream())
+
+
+def graph2tree(uv, n_ids, mode=capi.DEGREE_LLAMA, seq=None, parent=None, pst=None):
+    dev = uv.device
+    seq = seq if seq is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev)
+    parent = parent if parent is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev)
+    pst = pst if pst is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev)
+    n_seq = ctypes.c_uint32(0)
+    capi.call("sheep_graph2tree_dev", _p(uv), uv.shape[0], n_ids, mode, _p(seq), _p(parent),
+              _p(pst), ctypes.byref(n_seq), _stream())
+    return seq, parent, pst, n_seq.value

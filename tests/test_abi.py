@@ -1,0 +1,32 @@
+"""The C-ABI library loads (no GPU needed) and exports every symbol include/sheep_amd.h declares."""
+import subprocess
+
+from sheep_amd import capi
+
+
+def test_header_declares_expected_entry_points():
+    syms = capi.header_symbols()
+    for s in ("sheep_gpu_init", "sheep_degree_seq", "sheep_build_tree", "sheep_merge_trees",
+              "sheep_last_error", "sheep_graph2tree_dev", "sheep_merge_trees_dev"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    L = capi.lib()
+    for s in capi.header_symbols():
+        assert hasattr(L, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", capi.lib_path], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(capi.header_symbols()) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(capi.lib_path, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the offload bundle's target id
+
+
+def test_abi_version_and_error_text_without_gpu():
+    L = capi.lib()
+    assert L.sheep_abi_version() >> 16 == 1
+    assert isinstance(L.sheep_last_error(), bytes)

@@ -1,0 +1,165 @@
+"""GPU parity: libsheep_amd.so (HIP, gfx950) against the CPU checker, bit-exact.
+
+Inputs: the reference's hep-th fixture, the known-answer graph, seeded R-MAT streams (the GPU
+generator is itself checked against the host generator), random multigraphs with self-loops
+and duplicates, and the edge cases the reference defines (empty input, isolated ids, repeated
+seq ids, ids outside the sequence).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+PUB = json.load(open(os.path.join(GOLDEN, "hep_th_published.json")))
+KA = json.load(open(os.path.join(GOLDEN, "known_answer.json")))
+
+
+@pytest.fixture(scope="module")
+def api(gpu):
+    from sheep_amd import api
+
+    return api
+
+
+def check_tree(O, api, uv, seq):
+    t = api.build_tree(uv, seq)
+    p, s = O.build_tree(uv, seq)
+    assert np.array_equal(t.parent, p), "parent mismatch"
+    assert np.array_equal(t.pst, s), "pst mismatch"
+    return t
+
+
+def test_known_answer(oracle, api):
+    uv = np.array(KA["records"], np.uint32)
+    seq = api.degree_sequence(uv)
+    assert seq.tolist() == KA["llama_seq"]
+    t = api.build_tree(uv, seq)
+    assert [-1 if x == 0xFFFFFFFF else int(x) for x in t.parent] == KA["parent"]
+    assert t.pst.tolist() == KA["pst"]
+    assert api.degree_sequence(uv, api.DEGREE_FILE).tolist() == KA["file_seq_stream"]
+
+
+def test_hep_th_llama(oracle, api, hep_edges):
+    seq = api.degree_sequence(hep_edges)
+    assert np.array_equal(seq, oracle.degree_sequence(hep_edges))
+    t = check_tree(oracle, api, hep_edges, seq)
+    assert oracle.facts(t.parent, t.pst) == PUB["treefaqs"]
+
+
+def test_hep_th_file_mode_and_reader(oracle, api):
+    path = os.path.join(GOLDEN, "hep-th.dat")
+    fseq = api.file_sequence(path)
+    assert np.array_equal(fseq, oracle.degree_sequence(oracle.read_dat_xs1reader(path), oracle.FILE))
+    uv = api.read_dat(path)
+    t = check_tree(oracle, api, uv, fseq)
+    assert oracle.facts(t.parent, t.pst)["halo"] == 3530  # SURVEY A2 probe: FILE-mode seq
+
+
+@pytest.mark.parametrize("scale,seed", [(10, 1), (12, 2), (14, 3), (16, 4)])
+def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.rmat(scale, 16, seed)
+    uv = uv_d.cpu().numpy().view(np.uint32)
+    assert np.array_equal(uv, oracle.rmat(scale, 16, seed))
+    seq = api.degree_sequence(uv)
+    assert np.array_equal(seq, oracle.degree_sequence(uv))
+    check_tree(oracle, api, uv, seq)
+    # fused device pipeline
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << scale)
+    torch.cuda.synchronize()
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_multigraphs(oracle, api, seed):
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(2, 3000))
+    m = int(rng.integers(1, 20000))
+    uv = rng.integers(0, n, size=(m, 2)).astype(np.uint32)
+    dup = rng.integers(0, m, size=m // 10)
+    uv = np.concatenate([uv, uv[dup]])  # duplicate records (a multigraph, no DDUP_GRAPH)
+    loops = rng.random(m) < 0.03
+    uv[loops, 1] = uv[loops, 0]
+    for mode in (0, 1):
+        seq = api.degree_sequence(uv, mode)
+        assert np.array_equal(seq, oracle.degree_sequence(uv, mode))
+        check_tree(oracle, api, uv, seq)
+
+
+def test_random_seq_order(oracle, api):
+    """Any total order works (readSequence path, graph2tree.cpp:171-174)."""
+    uv = oracle.rmat(12, 8, 9)
+    seq = oracle.degree_sequence(uv)
+    rng = np.random.default_rng(5)
+    check_tree(oracle, api, uv, rng.permutation(seq).astype(np.uint32))
+
+
+def test_seq_subset_and_padding(oracle, api):
+    """Ids missing from seq behave as INVALID index (POSTORDER for their neighbours); seq may
+    carry ids with no edges (make_pad, jtree.h:88)."""
+    uv = np.array([[0, 1], [1, 2], [2, 3], [3, 0], [1, 3]], np.uint32)
+    seq = np.array([3, 1, 0, 7], np.uint32)  # 2 missing, 7 isolated
+    check_tree(oracle, api, uv, seq)
+
+
+def test_duplicate_seq_is_einval(api):
+    uv = np.array([[0, 1]], np.uint32)
+    with pytest.raises(api.SheepError) as e:
+        api.build_tree(uv, np.array([0, 1, 0], np.uint32))
+    assert e.value.code == -22
+
+
+def test_neighbour_beyond_seq_is_erange(api):
+    uv = np.array([[0, 1], [1, 5]], np.uint32)
+    with pytest.raises(api.SheepError) as e:
+        api.build_tree(uv, np.array([0, 1], np.uint32))
+    assert e.value.code == -34
+
+
+def test_empty_and_isolated(oracle, api):
+    assert api.degree_sequence(np.zeros((0, 2), np.uint32)).size == 0
+    uv = np.array([[5, 5]], np.uint32)  # only a self-loop: one vertex, no tree edge
+    seq = api.degree_sequence(uv)
+    assert seq.tolist() == [5]
+    t = check_tree(oracle, api, uv, seq)
+    assert t.parent.tolist() == [0xFFFFFFFF] and t.pst.tolist() == [0]
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 8])
+def test_merge_of_shards_equals_whole(oracle, api, k):
+    uv = oracle.rmat(14, 16, 11)
+    seq = oracle.degree_sequence(uv)
+    whole = oracle.build_tree(uv, seq)
+    R = len(uv)
+    trees = [api.build_tree(uv[R * i // k: R * (i + 1) // k], seq) for i in range(k)]
+    for i, t in enumerate(trees):  # each partial tree is itself exact
+        p, s = oracle.build_tree(uv[R * i // k: R * (i + 1) // k], seq)
+        assert np.array_equal(t.parent, p) and np.array_equal(t.pst, s)
+    step = 1
+    while step < k:  # pairwise log2 reduce, as scripts/reduce-worker.sh
+        for i in range(0, k - step, 2 * step):
+            a, b = trees[i], trees[i + step]
+            g = api.merge_trees(a, b)
+            p, s = oracle.merge(a.parent, a.pst, b.parent, b.pst)
+            assert np.array_equal(g.parent, p) and np.array_equal(g.pst, s)
+            trees[i] = g
+        step *= 2
+    assert np.array_equal(trees[0].parent, whole[0]) and np.array_equal(trees[0].pst, whole[1])
+
+
+def test_tre_roundtrip(api, hep_edges, tmp_path):
+    seq, t = api.graph2tree(hep_edges)
+    path = str(tmp_path / "h.tre")
+    t.save(path)
+    assert os.path.getsize(path) == 4 + 8 * len(seq)  # 60,884 B for hep-th
+    assert api.JNodeTable.load(path) == t
