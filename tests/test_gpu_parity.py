@@ -88,7 +88,7 @@ def test_random_multigraphs(oracle, api, seed):
     uv = rng.integers(0, n, size=(m, 2)).astype(np.uint32)
     dup = rng.integers(0, m, size=m // 10)
     uv = np.concatenate([uv, uv[dup]])  # duplicate records (a multigraph, no DDUP_GRAPH)
-    loops = rng.random(m) < 0.03
+    loops = rng.random(len(uv)) < 0.03
     uv[loops, 1] = uv[loops, 0]
     for mode in (0, 1):
         seq = api.degree_sequence(uv, mode)
