@@ -4,6 +4,8 @@
 // and returns a negative errno.  Device scratch is owned per device by a Ctx and grows on
 // demand; the hot path allocates nothing after its first call at a given size.
 #include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -186,8 +188,20 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const uint32_t* shi = which == 0 ? ka : hi;
   const uint32_t* slo = which == 0 ? va : lo;
   if (tm) tm->mark("bucket_sort");
-  launch_tree_insert(shi, slo, m, d_parent, jump, s);
+  const char* ev = getenv("SHEEP_TREE_VARIANT");
+  int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
+  const char* es = getenv("SHEEP_TREE_STATS");
+  bool stats = es && es[0] == '1';
+  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64);
+  launch_tree_insert(shi, slo, m, d_parent, jump, variant, stats, ws, s);
   if (tm) tm->mark("tree_insert");
+  if (stats) {
+    unsigned long long h[8];
+    HIP_CHECK(hipMemcpyAsync(h, ws, 64, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    fprintf(stderr, "tree_stats variant=%d edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
+            variant, h[1], h[2], h[3], h[4], h[5]);
+  }
 }
 
 }  // namespace sheep

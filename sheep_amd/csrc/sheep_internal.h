@@ -57,8 +57,10 @@ void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, ui
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                       uint32_t* pst, uint32_t* hi_out, uint32_t* lo_out, uint32_t* err,
                       hipStream_t s);
+// variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
 void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
-                        uint32_t* jump, hipStream_t s);
+                        uint32_t* jump, int variant, bool stats, unsigned long long* ws,
+                        hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

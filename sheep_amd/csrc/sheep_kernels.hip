@@ -356,62 +356,193 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 // edge — the same unique result as Liu's sequential union-find (jtree.cpp:73-83,
 // unionfind.h:46-102), independent of insertion order and interleaving.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ld_parent(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Parent loads.  LOAD 0: relaxed agent-scope atomic load (global_load sc1: bypasses L1, L2
+// served); 1: relaxed system-scope; 2: a returning atomic OR 0 (performed at memory, always
+// fresh).  Staleness never breaks correctness (see above), only costs extra CAS round trips.
+template <int LOAD>
+__device__ __forceinline__ uint32_t ld_parent(uint32_t* p) {
+  if (LOAD == 0) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (LOAD == 1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return atomicOr(p, 0u);
 }
 
-__device__ void zip_insert(uint32_t* __restrict__ parent, uint32_t* __restrict__ jump, uint32_t a,
-                           uint32_t b) {
-  uint32_t x = a, prev = INV, p = 0;
-  bool fresh = false;
-  for (;;) {
-    if (!fresh) {
-      uint32_t j = jump[x];
-      if (j > x && j < b) {
-        if (prev != INV) jump[prev] = j;
-        prev = x;
-        x = j;
-        continue;
+struct ZState {
+  uint32_t a, b, x, prev, p;
+  bool fresh;
+};
+
+struct ZCount {
+  uint32_t steps = 0, cas = 0, fail = 0;
+};
+
+// One step of the insertion of pending edge (s.a, s.b); returns true when it is finished.
+template <int LOAD, int JUMP, bool STATS>
+__device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZState& s, ZCount& c) {
+  if (STATS) c.steps++;
+  if (!s.fresh) {
+    if (JUMP) {
+      uint32_t j = jump[s.x];
+      if (j > s.x && j < s.b) {
+        if (s.prev != INV) jump[s.prev] = j;
+        s.prev = s.x;
+        s.x = j;
+        return false;
       }
-      p = ld_parent(&parent[x]);
     }
-    fresh = false;
-    if (p < b) {  // INVALID is never < b
-      if (prev != INV) jump[prev] = p;
-      prev = x;
-      x = p;
-      continue;
-    }
-    if (x != a) jump[a] = x;
-    if (p == b) return;
-    uint32_t old = atomicCAS(&parent[x], p, b);
-    if (old != p) {
-      p = old;
-      fresh = true;
-      continue;
-    }
-    if (p == INV) return;
-    a = b;
-    b = p;
-    x = a;
-    prev = INV;
+    s.p = ld_parent<LOAD>(&parent[s.x]);
   }
+  s.fresh = false;
+  if (s.p < s.b) {  // INVALID is never < b
+    if (JUMP && s.prev != INV) jump[s.prev] = s.p;
+    s.prev = s.x;
+    s.x = s.p;
+    return false;
+  }
+  if (JUMP && s.x != s.a) jump[s.a] = s.x;
+  if (s.p == s.b) return true;
+  if (STATS) c.cas++;
+  uint32_t old = atomicCAS(&parent[s.x], s.p, s.b);
+  if (old != s.p) {
+    if (STATS) c.fail++;
+    s.p = old;
+    s.fresh = true;
+    return false;
+  }
+  if (s.p == INV) return true;
+  s.a = s.b;  // zipper: continue with pending edge (b, old parent)
+  s.b = s.p;
+  s.x = s.a;
+  s.prev = INV;
+  return false;
 }
 
-__global__ void k_tree_insert(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
-                              uint64_t n, uint32_t* parent, uint32_t* jump) {
+__device__ __forceinline__ void zstart(ZState& s, uint32_t a, uint32_t b) {
+  s.a = a;
+  s.b = b;
+  s.x = a;
+  s.prev = INV;
+  s.fresh = false;
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(unsigned long long* stats, uint64_t edges, const ZCount& c,
+                                            uint32_t maxsteps) {
+  if (!STATS) return;
+  atomicAdd(&stats[0], (unsigned long long)edges);
+  atomicAdd(&stats[1], (unsigned long long)c.steps);
+  atomicAdd(&stats[2], (unsigned long long)c.cas);
+  atomicAdd(&stats[3], (unsigned long long)c.fail);
+  atomicMax(&stats[4], (unsigned long long)maxsteps);
+}
+
+// Variant A: one edge per thread per iteration, grid-stride (a wave waits for its slowest lane).
+template <int LOAD, int JUMP, bool STATS>
+__global__ void k_tree_loop(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                            uint64_t n, uint32_t* parent, uint32_t* jump,
+                            unsigned long long* next, unsigned long long* stats) {
+  ZCount c;
+  uint64_t edges = 0;
+  uint32_t maxsteps = 0;
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint32_t b = hi[i];
     if (b == INV) continue;
-    zip_insert(parent, jump, lo[i], b);
+    ZState s;
+    zstart(s, lo[i], b);
+    uint32_t st0 = c.steps;
+    while (!zip_step<LOAD, JUMP, STATS>(parent, jump, s, c)) {
+    }
+    if (STATS) { edges++; maxsteps = max(maxsteps, c.steps - st0); }
   }
+  flush_stats<STATS>(stats, edges, c, maxsteps);
 }
 
+// Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order from
+// one global counter (one atomic per 512 edges) and every lane that finishes an edge takes
+// the next one at the following step, so a wave never idles behind its slowest lane.
+template <int LOAD, int JUMP, bool STATS>
+__global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                             uint64_t n, uint32_t* parent, uint32_t* jump,
+                             unsigned long long* next, unsigned long long* stats) {
+  constexpr uint32_t CH = 64 * 8;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t cbase = 0, cend = 0;  // wave-uniform chunk cursor
+  bool active = false, exhausted = false;
+  ZState s;
+  ZCount c;
+  uint64_t edges = 0;
+  uint32_t maxsteps = 0, st0 = 0;
+  for (;;) {
+    uint64_t freem = __ballot(!active);
+    while (freem && !exhausted) {
+      if (cbase >= cend) {
+        unsigned long long st = 0;
+        if (lane == 0) st = atomicAdd(next, (unsigned long long)CH);
+        uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)st);
+        uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(st >> 32));
+        st = ((unsigned long long)hi32 << 32) | lo32;
+        if (st >= n) { exhausted = true; break; }
+        cbase = st;
+        cend = st + CH < n ? st + CH : n;
+      }
+      uint32_t k = (uint32_t)__popcll(freem & lt);
+      uint64_t cnt = (uint64_t)__popcll(freem);
+      uint64_t avail = cend - cbase;
+      if (!active && k < avail) {
+        uint64_t idx = cbase + k;
+        uint32_t b = hi[idx];
+        if (b != INV) {
+          zstart(s, lo[idx], b);
+          active = true;
+          if (STATS) { edges++; st0 = c.steps; }
+        }
+      }
+      cbase += cnt < avail ? cnt : avail;
+      freem = __ballot(!active);
+    }
+    if (__ballot(active) == 0) break;
+    if (active && zip_step<LOAD, JUMP, STATS>(parent, jump, s, c)) {
+      active = false;
+      if (STATS) maxsteps = max(maxsteps, c.steps - st0);
+    }
+  }
+  flush_stats<STATS>(stats, edges, c, maxsteps);
+}
+
+typedef void (*TreeKernel)(const uint32_t*, const uint32_t*, uint64_t, uint32_t*, uint32_t*,
+                           unsigned long long*, unsigned long long*);
+
+template <int LOAD, int JUMP, bool STATS>
+static TreeKernel pick_tree(int queue) {
+  return queue ? k_tree_queue<LOAD, JUMP, STATS> : k_tree_loop<LOAD, JUMP, STATS>;
+}
+
+template <bool STATS>
+static TreeKernel pick_tree(int load, int jmp, int queue) {
+  if (load == 0) return jmp ? pick_tree<0, 1, STATS>(queue) : pick_tree<0, 0, STATS>(queue);
+  if (load == 1) return jmp ? pick_tree<1, 1, STATS>(queue) : pick_tree<1, 0, STATS>(queue);
+  return jmp ? pick_tree<2, 1, STATS>(queue) : pick_tree<2, 0, STATS>(queue);
+}
+
+// variant = load + 4 * jump + 8 * queue; ws = 8 u64 words of device scratch (counter + stats).
 void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
-                        uint32_t* jump, hipStream_t s) {
+                        uint32_t* jump, int variant, bool stats, unsigned long long* ws,
+                        hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_tree_insert, dim3(grid_for(n)), dim3(BLOCK), 0, s, hi, lo, n, parent, jump);
+  int load = variant & 3, jmp = (variant >> 2) & 1, queue = (variant >> 3) & 1;
+  TreeKernel k = stats ? pick_tree<true>(load, jmp, queue) : pick_tree<false>(load, jmp, queue);
+  (void)hipMemsetAsync(ws, 0, 8 * sizeof(unsigned long long), s);
+  unsigned grid = queue ? (unsigned)MAX_GRID : grid_for(n);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, hi, lo, n, parent, jump, ws, ws + 1);
+}
+
+__device__ void zip_insert(uint32_t* parent, uint32_t* jump, uint32_t a, uint32_t b) {
+  ZState s;
+  ZCount c;
+  zstart(s, a, b);
+  while (!zip_step<0, 1, false>(parent, jump, s, c)) {
+  }
 }
 
 // Merge (jnode.cpp:174-201): insert every edge (v, parent_b[v]) of tree B into tree A;
