@@ -13,7 +13,7 @@ from sheep_amd import capi, device  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scale", type=int, default=24)
-ap.add_argument("--variants", default="4,12,0,8,5,13,6,14")
+ap.add_argument("--variants", default="zip:12,kb:128,kb:512,kb:2048")
 ap.add_argument("--reps", type=int, default=2)
 args = ap.parse_args()
 device.init(0)
@@ -24,8 +24,10 @@ seq, rank, n_seq = device.sequence(deg)
 torch.cuda.synchronize()
 print("scale", S, "records", uv.shape[0], "n_seq", n_seq, flush=True)
 ref = None
-for v in [int(x) for x in args.variants.split(",")]:
-    os.environ["SHEEP_TREE_VARIANT"] = str(v)
+for v in args.variants.split(","):
+    algo, knob = v.split(":")
+    os.environ["SHEEP_TREE_ALGO"] = algo
+    os.environ["SHEEP_TREE_VARIANT" if algo == "zip" else "SHEEP_KB_BUCKETS"] = knob
     os.environ["SHEEP_TREE_STATS"] = "0"
     best = 1e9
     for _ in range(args.reps):
@@ -42,5 +44,5 @@ for v in [int(x) for x in args.variants.split(",")]:
     os.environ["SHEEP_TREE_STATS"] = "1"
     device.build_tree(uv, rank, n_seq)
     torch.cuda.synchronize()
-    print("variant %2d tree_insert %.2f ms  other %s  same=%s" % (
+    print("variant %s tree_insert %.2f ms  other %s  same=%s" % (
         v, best, {k: round(x, 2) for k, x in ph.items() if k != "tree_insert"}, same), flush=True)

@@ -180,27 +180,58 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint32_t* tmp = (uint32_t*)c.scratch.get("radix_tmp", radix_tmp_words(m) * 4);
   launch_edge_pass(d_uv, m, d_rank, n_rank, d_pst, hi, lo, c.d_err, s);
   if (tm) tm->mark("edge_pass");
-  // Bucket the tree edges by the top 16 bits of hi (approximate Liu order; exactness does not
-  // depend on the order, only the amount of zipper work does).
+  const char* ea = getenv("SHEEP_TREE_ALGO");
+  bool kb = !(ea && strcmp(ea, "zip") == 0);
+  const char* es = getenv("SHEEP_TREE_STATS");
+  bool stats = es && es[0] == '1';
   int top = bits_for(n_seq);
-  int lo_bit = std::max(0, top - 16);
+  // kb needs edges fully sorted by hi (bucket ranges + wave dedupe); the plain zipper only
+  // needs them bucketed by the top 16 bits (order affects work, never the result).
+  int lo_bit = kb ? 0 : std::max(0, top - 16);
   int which = radix_sort_pairs(hi, lo, ka, va, hi, lo, m, lo_bit, top, tmp, s);
   const uint32_t* shi = which == 0 ? ka : hi;
   const uint32_t* slo = which == 0 ? va : lo;
   if (tm) tm->mark("bucket_sort");
-  const char* ev = getenv("SHEEP_TREE_VARIANT");
-  int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
-  const char* es = getenv("SHEEP_TREE_STATS");
-  bool stats = es && es[0] == '1';
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64);
-  launch_tree_insert(shi, slo, m, d_parent, jump, variant, stats, ws, s);
+  if (!kb) {
+    const char* ev = getenv("SHEEP_TREE_VARIANT");
+    int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
+    launch_tree_insert(shi, slo, m, d_parent, jump, variant, stats, ws, s);
+  } else {
+    const char* ek = getenv("SHEEP_KB_BUCKETS");
+    uint32_t K = ek ? (uint32_t)atoi(ek) : 512;
+    uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
+    uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
+    uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
+    uint32_t* n_linked = (uint32_t*)c.scratch.get("kb_nlinked", 16);
+    unsigned long long* bounds =
+        (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
+    launch_iota(uf, n_seq, s);
+    launch_iota(label, n_seq, s);
+    (void)hipMemsetAsync(n_linked, 0, 16, s);
+    (void)hipMemsetAsync(ws, 0, 64, s);
+    launch_kb_bounds(shi, m, K, bounds, s);
+    std::vector<unsigned long long> hb(2 * (K + 1));
+    HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (tm) tm->mark("kb_bounds");
+    uint64_t m_valid = hb[2 * K + 1];
+    // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
+    std::vector<std::pair<uint32_t, uint64_t>> bk;
+    for (uint32_t k = 0; k < K; ++k)
+      if (bk.empty() || (uint32_t)hb[2 * k] > bk.back().first) bk.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
+    bk.emplace_back(n_seq, m_valid);
+    for (size_t k = 0; k + 1 < bk.size(); ++k)
+      launch_kb_bucket(shi, slo, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
+                       label, d_parent, jump, linked, n_linked, stats, ws + 1, s);
+  }
   if (tm) tm->mark("tree_insert");
   if (stats) {
     unsigned long long h[8];
     HIP_CHECK(hipMemcpyAsync(h, ws, 64, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    fprintf(stderr, "tree_stats variant=%d edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
-            variant, h[1], h[2], h[3], h[4], h[5]);
+    fprintf(stderr, "tree_stats algo=%s edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu kept=%llu\n",
+            kb ? "kb" : "zip", h[1], h[2], h[3], h[4], h[5], h[6]);
   }
 }
 

@@ -545,6 +545,215 @@ __device__ void zip_insert(uint32_t* parent, uint32_t* jump, uint32_t a, uint32_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Bucket-synchronous Kruskal ("kb"): Liu's algorithm run over rank buckets [B0, B1) in order.
+//
+// Between buckets the connectivity of every edge with hi < B0 is held in a union-find uf[]
+// (random-priority linking, path halving) whose roots carry label[] = the component's max
+// jnid = its elimination-tree root.  Both are frozen (and coherent: kernel boundary) while a
+// bucket runs, so for a tree edge (a, b) with a < B0 the walk of Liu's find is replaced by
+//     g = label[find(a)]     (exact: g < B0 <= b and a ~ g through vertices <= g)
+// (a >= B0: g = a).  Inside a wave the 64 consecutive edges (sorted by b) are deduplicated on
+// (g, b) — a hub's thousands of edges from the giant component collapse to one — and the
+// survivors are inserted with the lock-free zipper, whose walks now stay inside the bucket.
+// After the bucket: union(x, parent[x]) for every link the bucket created (pre-bucket roots
+// that were linked are recorded by the zipper), then label[find(v)] = v for every in-bucket
+// etree root v.  The result is the unique etree, as for the plain zipper.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t uf_prio(uint32_t x) {  // a bijection on u32: no ties
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// find with path halving.  ATOMIC: loads with relaxed agent atomics (during concurrent unions).
+template <bool ATOMIC>
+__device__ __forceinline__ uint32_t uf_find(uint32_t* uf, uint32_t x) {
+  for (;;) {
+    uint32_t p = ATOMIC ? __hip_atomic_load(&uf[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : uf[x];
+    if (p == x) return x;
+    uint32_t gp = ATOMIC ? __hip_atomic_load(&uf[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : uf[p];
+    if (gp == p) return p;
+    uf[x] = gp;  // x is a non-root forever; any ancestor is a valid pointer
+    x = gp;
+  }
+}
+
+__device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v) {
+  for (;;) {
+    uint32_t ru = uf_find<true>(uf, u), rv = uf_find<true>(uf, v);
+    if (ru == rv) return;
+    if (uf_prio(ru) > uf_prio(rv)) { uint32_t t = ru; ru = rv; rv = t; }
+    if (atomicCAS(&uf[ru], ru, rv) == ru) return;
+  }
+}
+
+// Zipper insertion that records pre-bucket roots (x < B0) it links for the first time.
+__device__ __forceinline__ void zip_insert_rec(uint32_t* parent, uint32_t* jump, uint32_t a,
+                                               uint32_t b, uint32_t B0, uint32_t* linked,
+                                               uint32_t* n_linked, ZCount& c) {
+  ZState s;
+  zstart(s, a, b);
+  for (;;) {
+    c.steps++;
+    if (!s.fresh) {
+      uint32_t j = jump[s.x];
+      if (j > s.x && j < s.b) {
+        if (s.prev != INV) jump[s.prev] = j;
+        s.prev = s.x;
+        s.x = j;
+        continue;
+      }
+      s.p = ld_parent<0>(&parent[s.x]);
+    }
+    s.fresh = false;
+    if (s.p < s.b) {
+      if (s.prev != INV) jump[s.prev] = s.p;
+      s.prev = s.x;
+      s.x = s.p;
+      continue;
+    }
+    if (s.x != s.a) jump[s.a] = s.x;
+    if (s.p == s.b) return;
+    c.cas++;
+    uint32_t old = atomicCAS(&parent[s.x], s.p, s.b);
+    if (old != s.p) {
+      c.fail++;
+      s.p = old;
+      s.fresh = true;
+      continue;
+    }
+    if (s.p == INV) {
+      if (s.x < B0) linked[atomicAdd(n_linked, 1u)] = s.x;
+      return;
+    }
+    s.a = s.b;
+    s.b = s.p;
+    s.x = s.a;
+    s.prev = INV;
+  }
+}
+
+template <bool STATS>
+__global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                         uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
+                         const uint32_t* __restrict__ label, uint32_t* parent, uint32_t* jump,
+                         uint32_t* linked, uint32_t* n_linked, unsigned long long* stats) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  ZCount c;
+  uint64_t edges = 0, kept = 0;
+  for (uint64_t base = e_begin + wave * 64; base < e_end; base += nwaves * 64) {
+    uint64_t idx = base + lane;
+    bool valid = idx < e_end;
+    uint32_t b = valid ? hi[idx] : INV;
+    uint32_t a = valid ? lo[idx] : 0;
+    uint32_t g = a;
+    if (valid && a < B0) g = label[uf_find<false>(uf, a)];
+    // keep the first lane of every distinct (g, b) in the wave
+    bool keep = valid;
+    uint64_t rem = __ballot(valid);
+    while (rem) {
+      int leader = __ffsll((unsigned long long)rem) - 1;
+      uint32_t lb = __builtin_amdgcn_readlane(b, leader);
+      uint32_t lg = __builtin_amdgcn_readlane(g, leader);
+      uint64_t same = __ballot(valid && b == lb && g == lg);
+      if (lane != leader && ((same >> lane) & 1)) keep = false;
+      rem &= ~same;
+    }
+    if (STATS) { edges += valid; kept += keep; }
+    if (keep) zip_insert_rec(parent, jump, g, b, B0, linked, n_linked, c);
+  }
+  if (STATS) {
+    atomicAdd(&stats[0], (unsigned long long)edges);
+    atomicAdd(&stats[1], (unsigned long long)c.steps);
+    atomicAdd(&stats[2], (unsigned long long)c.cas);
+    atomicAdd(&stats[3], (unsigned long long)c.fail);
+    atomicAdd(&stats[5], (unsigned long long)kept);
+  }
+}
+
+__global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
+                           uint32_t B1, const uint32_t* __restrict__ linked,
+                           const uint32_t* __restrict__ n_linked) {
+  const uint32_t nl = *n_linked, width = B1 - B0;
+  const uint64_t total = (uint64_t)width + nl;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v = i < width ? B0 + (uint32_t)i : linked[i - width];
+    uint32_t p = parent[v];
+    if (p != INV) uf_union(uf, v, p);
+  }
+}
+
+__global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
+                           uint32_t B0, uint32_t B1, uint32_t* n_linked) {
+  for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
+    if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_linked = 0;
+}
+
+// Bucket boundaries by edge count: thread k finds m_valid (first INVALID hi), takes the rank at
+// position k*m_valid/K and lower_bounds it.  out[2k] = B_k, out[2k+1] = first edge of bucket k.
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t n, uint32_t key) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_kb_bounds(const uint32_t* __restrict__ hi, uint64_t n, uint32_t K,
+                            unsigned long long* out) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > K) return;
+  uint64_t mv = lower_bound_u32(hi, n, INV);
+  if (k == K) { out[2 * K] = INV; out[2 * K + 1] = mv; return; }
+  uint64_t pos = mv * k / K;
+  uint32_t B = (k == 0 || mv == 0) ? 0u : hi[pos];
+  out[2 * k] = B;
+  out[2 * k + 1] = lower_bound_u32(hi, mv, B);
+}
+
+void launch_kb_bounds(const uint32_t* hi, uint64_t n, uint32_t K, unsigned long long* out,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_kb_bounds, dim3((K + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, hi, n, K, out);
+}
+
+void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, uint64_t e_end,
+                      uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
+                      uint32_t* jump, uint32_t* linked, uint32_t* n_linked, bool stats,
+                      unsigned long long* st, hipStream_t s) {
+  if (e_end > e_begin) {
+    uint64_t waves = (e_end - e_begin + 63) / 64;
+    unsigned grid = grid_for(waves * 64);
+    if (stats)
+      hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
+                         uf, (const uint32_t*)label, parent, jump, linked, n_linked, st);
+    else
+      hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
+                         uf, (const uint32_t*)label, parent, jump, linked, n_linked, st);
+  }
+  unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
+  hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
+                     (const uint32_t*)linked, (const uint32_t*)n_linked);
+  hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
+                     (const uint32_t*)parent, uf, label, B0, B1, n_linked);
+}
+
+__global__ void k_iota(uint32_t* p, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = i;
+}
+
+void launch_iota(uint32_t* p, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(BLOCK), 0, s, p, n);
+}
+
 // Merge (jnode.cpp:174-201): insert every edge (v, parent_b[v]) of tree B into tree A;
 // pst_weight sums (u32 wrap-around, as the reference's esize_t += ).
 __global__ void k_merge(uint32_t* parent_a, uint32_t* __restrict__ pst_a,
