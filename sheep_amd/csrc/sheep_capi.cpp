@@ -192,24 +192,26 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const uint32_t* shi = which == 0 ? ka : hi;
   const uint32_t* slo = which == 0 ? va : lo;
   if (tm) tm->mark("bucket_sort");
-  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64);
+  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   if (!kb) {
     const char* ev = getenv("SHEEP_TREE_VARIANT");
     int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
     launch_tree_insert(shi, slo, m, d_parent, jump, variant, stats, ws, s);
   } else {
     const char* ek = getenv("SHEEP_KB_BUCKETS");
-    uint32_t K = ek ? (uint32_t)atoi(ek) : 512;
+    uint32_t K = ek ? (uint32_t)atoi(ek) : 16;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
     uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
-    uint32_t* n_linked = (uint32_t*)c.scratch.get("kb_nlinked", 16);
+    uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 16);
+    // the sort's free ping-pong pair holds the kept (b, g) list of a bucket
+    uint32_t* kept_b = which == 0 ? hi : ka;
+    uint32_t* kept_g = which == 0 ? lo : va;
     unsigned long long* bounds =
         (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
     launch_iota(uf, n_seq, s);
     launch_iota(label, n_seq, s);
-    (void)hipMemsetAsync(n_linked, 0, 16, s);
-    (void)hipMemsetAsync(ws, 0, 64, s);
+    (void)hipMemsetAsync(ws, 0, 64 * 2, s);
     launch_kb_bounds(shi, m, K, bounds, s);
     std::vector<unsigned long long> hb(2 * (K + 1));
     HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
@@ -223,15 +225,19 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     bk.emplace_back(n_seq, m_valid);
     for (size_t k = 0; k + 1 < bk.size(); ++k)
       launch_kb_bucket(shi, slo, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
-                       label, d_parent, jump, linked, n_linked, stats, ws + 1, s);
+                       label, d_parent, jump, kept_b, kept_g, linked, counters, stats, ws, s);
   }
   if (tm) tm->mark("tree_insert");
   if (stats) {
-    unsigned long long h[8];
-    HIP_CHECK(hipMemcpyAsync(h, ws, 64, hipMemcpyDeviceToHost, s));
+    unsigned long long h[16];
+    HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    fprintf(stderr, "tree_stats algo=%s edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu kept=%llu\n",
-            kb ? "kb" : "zip", h[1], h[2], h[3], h[4], h[5], h[6]);
+    if (kb)
+      fprintf(stderr, "tree_stats algo=kb edges=%llu kept=%llu zip_edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
+              h[0], h[5], h[8], h[9], h[10], h[11], h[12]);
+    else
+      fprintf(stderr, "tree_stats algo=zip edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
+              h[1], h[2], h[3], h[4], h[5]);
   }
 }
 

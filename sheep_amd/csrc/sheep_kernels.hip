@@ -376,8 +376,15 @@ struct ZCount {
 };
 
 // One step of the insertion of pending edge (s.a, s.b); returns true when it is finished.
-template <int LOAD, int JUMP, bool STATS>
-__device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZState& s, ZCount& c) {
+struct ZRec {  // where to record pre-bucket roots (x < B0) that a CAS links for the first time
+  uint32_t B0 = 0;
+  uint32_t* linked = nullptr;
+  uint32_t* n_linked = nullptr;
+};
+
+template <int LOAD, int JUMP, bool STATS, bool REC = false>
+__device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZState& s, ZCount& c,
+                                         const ZRec& rec = ZRec()) {
   if (STATS) c.steps++;
   if (!s.fresh) {
     if (JUMP) {
@@ -408,7 +415,10 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
     s.fresh = true;
     return false;
   }
-  if (s.p == INV) return true;
+  if (s.p == INV) {
+    if (REC && s.x < rec.B0) rec.linked[atomicAdd(rec.n_linked, 1u)] = s.x;
+    return true;
+  }
   s.a = s.b;  // zipper: continue with pending edge (b, old parent)
   s.b = s.p;
   s.x = s.a;
@@ -460,10 +470,12 @@ __global__ void k_tree_loop(const uint32_t* __restrict__ hi, const uint32_t* __r
 // Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order from
 // one global counter (one atomic per 512 edges) and every lane that finishes an edge takes
 // the next one at the following step, so a wave never idles behind its slowest lane.
-template <int LOAD, int JUMP, bool STATS>
-__global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
-                             uint64_t n, uint32_t* parent, uint32_t* jump,
-                             unsigned long long* next, unsigned long long* stats) {
+template <int LOAD, int JUMP, bool STATS, bool REC>
+__device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
+                                                const uint32_t* __restrict__ lo, uint64_t n,
+                                                uint32_t* parent, uint32_t* jump,
+                                                unsigned long long* next, unsigned long long* stats,
+                                                const ZRec& rec) {
   constexpr uint32_t CH = 64 * 8;
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -502,12 +514,33 @@ __global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __
       freem = __ballot(!active);
     }
     if (__ballot(active) == 0) break;
-    if (active && zip_step<LOAD, JUMP, STATS>(parent, jump, s, c)) {
+    if (active && zip_step<LOAD, JUMP, STATS, REC>(parent, jump, s, c, rec)) {
       active = false;
       if (STATS) maxsteps = max(maxsteps, c.steps - st0);
     }
   }
   flush_stats<STATS>(stats, edges, c, maxsteps);
+}
+
+template <int LOAD, int JUMP, bool STATS>
+__global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                             uint64_t n, uint32_t* parent, uint32_t* jump,
+                             unsigned long long* next, unsigned long long* stats) {
+  tree_queue_body<LOAD, JUMP, STATS, false>(hi, lo, n, parent, jump, next, stats, ZRec());
+}
+
+// The kb in-bucket pass: the kept (g, b) list of a bucket (count on the device) through the
+// balanced lane queue, recording pre-bucket roots it links.
+template <bool STATS>
+__global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
+                         const uint32_t* __restrict__ n_kept, uint32_t* parent, uint32_t* jump,
+                         unsigned long long* next, unsigned long long* stats, uint32_t B0,
+                         uint32_t* linked, uint32_t* n_linked) {
+  ZRec rec;
+  rec.B0 = B0;
+  rec.linked = linked;
+  rec.n_linked = n_linked;
+  tree_queue_body<0, 1, STATS, true>(kb, kg, *n_kept, parent, jump, next, stats, rec);
 }
 
 typedef void (*TreeKernel)(const uint32_t*, const uint32_t*, uint64_t, uint32_t*, uint32_t*,
@@ -640,8 +673,8 @@ __device__ __forceinline__ void zip_insert_rec(uint32_t* parent, uint32_t* jump,
 template <bool STATS>
 __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
                          uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
-                         const uint32_t* __restrict__ label, uint32_t* parent, uint32_t* jump,
-                         uint32_t* linked, uint32_t* n_linked, unsigned long long* stats) {
+                         const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
+                         uint32_t* n_kept, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -666,7 +699,15 @@ __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __rest
       rem &= ~same;
     }
     if (STATS) { edges += valid; kept += keep; }
-    if (keep) zip_insert_rec(parent, jump, g, b, B0, linked, n_linked, c);
+    uint64_t km = __ballot(keep);
+    uint32_t slot = 0;
+    if (lane == 0 && km) slot = atomicAdd(n_kept, (uint32_t)__popcll(km));
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    if (keep) {
+      uint32_t pos = slot + (uint32_t)__popcll(km & (lane ? (~0ull >> (64 - lane)) : 0ull));
+      kept_b[pos] = b;
+      kept_g[pos] = g;
+    }
   }
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
@@ -727,17 +768,31 @@ void launch_kb_bounds(const uint32_t* hi, uint64_t n, uint32_t K, unsigned long 
 
 void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
-                      uint32_t* jump, uint32_t* linked, uint32_t* n_linked, bool stats,
-                      unsigned long long* st, hipStream_t s) {
+                      uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
+                      uint32_t* counters, bool stats, unsigned long long* st, hipStream_t s) {
+  // counters: [0] n_kept, [1] n_linked, [2..3] u64 queue cursor
+  uint32_t* n_kept = counters;
+  uint32_t* n_linked = counters + 1;
+  unsigned long long* next = (unsigned long long*)(counters + 2);
   if (e_end > e_begin) {
     uint64_t waves = (e_end - e_begin + 63) / 64;
     unsigned grid = grid_for(waves * 64);
-    if (stats)
+    (void)hipMemsetAsync(counters, 0, 16, s);
+    if (stats) {
       hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, parent, jump, linked, n_linked, st);
-    else
+                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st);
+      hipLaunchKernelGGL(k_kb_zip<true>, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
+                         (const uint32_t*)kept_g, (const uint32_t*)n_kept, parent, jump, next, st + 8,
+                         B0, linked, n_linked);
+    } else {
       hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, parent, jump, linked, n_linked, st);
+                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st);
+      hipLaunchKernelGGL(k_kb_zip<false>, dim3(MAX_GRID), dim3(BLOCK), 0, s,
+                         (const uint32_t*)kept_b, (const uint32_t*)kept_g, (const uint32_t*)n_kept,
+                         parent, jump, next, st + 8, B0, linked, n_linked);
+    }
+  } else {
+    (void)hipMemsetAsync(counters, 0, 16, s);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
