@@ -140,6 +140,19 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 
 // ---- device-level building blocks ---------------------------------------------------------
 
+// Degree: LDS-bucketed histogram for large inputs, global atomics for small ones.
+static void degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
+                       uint32_t* d_deg, hipStream_t s) {
+  const char* e = getenv("SHEEP_DEGREE");
+  bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
+  if (!bucketed || n_ids == 0) {
+    launch_degree(d_uv, m, n_ids, mode, d_deg, c.d_err, s);
+    return;
+  }
+  uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
+  launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, nullptr, c.d_err, tmp, s);
+}
+
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
                              uint32_t* d_rank, hipStream_t s) {
   if (n_ids == 0) return 0;
@@ -310,7 +323,7 @@ int sheep_degree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degre
   require_aligned(d_uv, "d_uv");
   if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
     throw ApiError(-EINVAL, "degree_mode");
-  launch_degree(d_uv, m, n_ids, degree_mode, d_deg, c.d_err, pick(c, stream));
+  degree_dev(c, d_uv, m, n_ids, degree_mode, d_deg, pick(c, stream));
   API_END
 }
 
@@ -358,7 +371,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   Timer tm(s);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
-  launch_degree(d_uv, m, n_ids, degree_mode, deg, c.d_err, s);
+  degree_dev(c, d_uv, m, n_ids, degree_mode, deg, s);
   tm.mark("degree");
   uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
   tm.mark("sequence");
@@ -395,7 +408,7 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
   uint32_t* seq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_ids * 4);
-  launch_degree(uv, m, n_ids, degree_mode, deg, c.d_err, s);
+  degree_dev(c, uv, m, n_ids, degree_mode, deg, s);
   check_err(c, s);
   uint32_t n_seq = sequence_dev(c, deg, n_ids, seq, rank, s);
   if (n_seq) HIP_CHECK(hipMemcpyAsync(seq_out, seq, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));

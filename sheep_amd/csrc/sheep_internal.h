@@ -38,6 +38,11 @@ Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)
 // ---- launchers (sheep_kernels.hip); all enqueue on `s` -------------------------------------
 void launch_degree(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
                    uint32_t* err, hipStream_t s);
+// Bucketed LDS degree histogram for large m (same result as launch_degree); selfc nullable.
+size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out);
+void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+                            uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
+                            hipStream_t s);
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max,[1]=zeros*/,
                       hipStream_t s);
 // Exclusive scan of n u32 (n < 2^32); tmp needs scan_tmp_words(n) u32.
