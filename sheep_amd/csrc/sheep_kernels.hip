@@ -13,6 +13,7 @@
 //   k_merge         associative tree union (jnode.cpp:174-201) with the same insertion
 //   k_rmat          synthetic input generator (rmat.h)
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "rmat.h"
 #include "sheep_internal.h"
@@ -843,7 +844,7 @@ template <bool STATS>
 __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
                          uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
                          const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
-                         uint32_t* n_kept, unsigned long long* stats) {
+                         uint32_t* n_kept, unsigned long long* stats, int mapmode) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -855,10 +856,10 @@ __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __rest
     uint32_t b = valid ? hi[idx] : INV;
     uint32_t a = valid ? lo[idx] : 0;
     uint32_t g = a;
-    if (valid && a < B0) g = label[uf_find<false>(uf, a)];
+    if (valid && a < B0 && mapmode != 2) g = label[uf_find<false>(uf, a)];
     // keep the first lane of every distinct (g, b) in the wave
     bool keep = valid;
-    uint64_t rem = __ballot(valid);
+    uint64_t rem = mapmode == 1 ? 0ull : __ballot(valid);
     while (rem) {
       int leader = __ffsll((unsigned long long)rem) - 1;
       uint32_t lb = __builtin_amdgcn_readlane(b, leader);
@@ -939,6 +940,8 @@ void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, 
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
                       uint32_t* counters, bool stats, unsigned long long* st, hipStream_t s) {
+  const char* em = getenv("SHEEP_KB_MAPMODE");
+  int mapmode = em ? atoi(em) : 0;
   // counters: [0] n_kept, [1] n_linked, [2..3] u64 queue cursor
   uint32_t* n_kept = counters;
   uint32_t* n_linked = counters + 1;
@@ -949,13 +952,13 @@ void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, 
     (void)hipMemsetAsync(counters, 0, 16, s);
     if (stats) {
       hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st);
+                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<true>, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
                          (const uint32_t*)kept_g, (const uint32_t*)n_kept, parent, jump, next, st + 8,
                          B0, linked, n_linked);
     } else {
       hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st);
+                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<false>, dim3(MAX_GRID), dim3(BLOCK), 0, s,
                          (const uint32_t*)kept_b, (const uint32_t*)kept_g, (const uint32_t*)n_kept,
                          parent, jump, next, st + 8, B0, linked, n_linked);
