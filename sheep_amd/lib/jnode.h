@@ -1,0 +1,139 @@
+// The tree (reference: lib/jnode.h:45-298, lib/jnode.cpp).  JNode = {jnid_t parent,
+// esize_t pst_weight}; INVALID parent = root.  The table lives in host memory; construction
+// (JTree) and merge run on the GPU through the C-ABI.  .tre = u32 end_id, then max_id JNodes.
+#pragma once
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+#include <stdexcept>
+#include <vector>
+
+#include "defs.h"
+#include "sheep_call.h"
+
+class JNodeTable {
+ public:
+  struct JNode {
+    jnid_t parent;
+    esize_t pst_weight;
+  };
+
+ private:
+  std::vector<JNode> nodes_;
+  jnid_t end_id_ = 0;
+  std::vector<uint64_t> kid_off_;  // makeKids (jnode.h:190-204): ascending jnid order
+  std::vector<jnid_t> kid_ids_;
+
+ public:
+  JNodeTable() = default;
+  explicit JNodeTable(jnid_t max_jnids) : nodes_(max_jnids, JNode{INVALID_JNID, 0}), end_id_(max_jnids) {}
+  JNodeTable(std::vector<jnid_t> const& parent, std::vector<esize_t> const& pst) {
+    nodes_.resize(parent.size());
+    for (size_t i = 0; i < parent.size(); ++i) nodes_[i] = JNode{parent[i], pst[i]};
+    end_id_ = (jnid_t)parent.size();
+  }
+  // Open constructor (jnode.cpp:76-102): max_id from the file size, end_id from the header,
+  // then makeKids.
+  explicit JNodeTable(char const* filename) {
+    std::ifstream s(filename, std::ios::binary | std::ios::ate);
+    if (!s) throw std::bad_alloc();
+    size_t bytes = (size_t)s.tellg();
+    s.seekg(0);
+    if (bytes < sizeof(jnid_t)) throw std::bad_alloc();
+    s.read((char*)&end_id_, sizeof(jnid_t));
+    nodes_.resize((bytes - sizeof(jnid_t)) / sizeof(JNode));
+    s.read((char*)nodes_.data(), nodes_.size() * sizeof(JNode));
+    makeKids();
+  }
+
+  jnid_t size() const { return end_id_; }
+  jnid_t& parent(jnid_t id) { return nodes_[id].parent; }
+  jnid_t parent(jnid_t id) const { return nodes_[id].parent; }
+  esize_t& pst_weight(jnid_t id) { return nodes_[id].pst_weight; }
+  esize_t pst_weight(jnid_t id) const { return nodes_[id].pst_weight; }
+  size_t width(jnid_t id) const { return 1 + (size_t)nodes_[id].pst_weight; }  // jnode.h:258-260
+
+  std::vector<jnid_t> parents() const {
+    std::vector<jnid_t> p(end_id_);
+    for (jnid_t i = 0; i < end_id_; ++i) p[i] = nodes_[i].parent;
+    return p;
+  }
+  std::vector<esize_t> psts() const {
+    std::vector<esize_t> w(end_id_);
+    for (jnid_t i = 0; i < end_id_; ++i) w[i] = nodes_[i].pst_weight;
+    return w;
+  }
+
+  // save (jnode.cpp:164-168)
+  void save(char const* filename) const {
+    std::ofstream s(filename, std::ios::binary | std::ios::trunc);
+    s.write((const char*)&end_id_, sizeof(jnid_t));
+    s.write((const char*)nodes_.data(), nodes_.size() * sizeof(JNode));
+  }
+
+  // merge (jnode.cpp:174-201) on the GPU: *this <- etree(lhs ∪ rhs), pst summed.
+  void merge(JNodeTable const& lhs, JNodeTable const& rhs) {
+    if (lhs.size() != rhs.size()) throw std::invalid_argument("merge: tables of different size");
+    jnid_t n = lhs.size();
+    std::vector<jnid_t> pa = lhs.parents(), pb = rhs.parents(), po(n);
+    std::vector<esize_t> sa = lhs.psts(), sb = rhs.psts(), so(n);
+    if (n) sheep_check(sheep_merge_trees(pa.data(), sa.data(), pb.data(), sb.data(), n, po.data(), so.data()), "merge");
+    *this = JNodeTable(po, so);
+  }
+
+  void makeKids() {
+    kid_off_.assign((size_t)end_id_ + 1, 0);
+    for (jnid_t id = 0; id < end_id_; ++id)
+      if (parent(id) != INVALID_JNID) kid_off_.at(parent(id) + 1)++;
+    for (jnid_t id = 0; id < end_id_; ++id) kid_off_[id + 1] += kid_off_[id];
+    kid_ids_.resize(kid_off_[end_id_]);
+    std::vector<uint64_t> pos(kid_off_.begin(), kid_off_.end() - 1);
+    for (jnid_t id = 0; id < end_id_; ++id)
+      if (parent(id) != INVALID_JNID) kid_ids_[pos[parent(id)]++] = id;
+  }
+  bool hasKids() const { return kid_off_.size() == (size_t)end_id_ + 1; }
+  jnid_t* kids_begin(jnid_t id) { return kid_ids_.data() + kid_off_[id]; }
+  jnid_t* kids_end(jnid_t id) { return kid_ids_.data() + kid_off_[id + 1]; }
+
+  // Facts (jnode.cpp:256-290; print jnode.h:285-291)
+  struct Facts {
+    size_t vert_cnt = 0, edge_cnt = 0, width = 0, fill = 0, vert_height = 0, edge_height = 0,
+           root_cnt = 0;
+    jnid_t halo_id = INVALID_JNID, core_id = INVALID_JNID;
+    explicit Facts(JNodeTable const& jn) {
+      std::vector<unsigned long long> vh(jn.size(), 0), eh(jn.size(), 0);
+      for (jnid_t id = 0; id != jn.size(); ++id) {
+        jnid_t p = jn.parent(id);
+        vert_cnt++;
+        edge_cnt += jn.pst_weight(id);
+        width = std::max(width, jn.width(id));
+        fill += jn.width(id) - jn.pst_weight(id) - 1;
+        vh[id]++;
+        eh[id] += jn.pst_weight(id);
+        if (p != INVALID_JNID) {
+          vh.at(p) = std::max(vh[p], vh[id]);
+          eh.at(p) = std::max(eh[p], eh[id]);
+        } else {
+          vert_height = std::max<size_t>(vert_height, vh[id]);
+          edge_height = std::max<size_t>(edge_height, eh[id]);
+          root_cnt++;
+        }
+        if (halo_id == INVALID_JNID && jn.width(id) > 3) halo_id = id;
+        if (core_id == INVALID_JNID && jn.width(id) >= width) core_id = id;
+      }
+    }
+    void print() const {
+      printf("TREEFAQS: width:%zu\troots:%zu\n", width, root_cnt);
+      printf("\tvheight:%zu\teheight:%zu\n", vert_height, edge_height);
+      printf("\tverts:%zu\tedges:%zu\n", vert_cnt, edge_cnt);
+      printf("\thalo:%zu\tcore:%zu\n", (size_t)halo_id, (size_t)core_id);
+      printf("\tfill:%zu\n", fill);
+    }
+  };
+  Facts getFacts() const { return Facts(*this); }
+
+  void print(jnid_t id) const {  // jnode.h:264-267 (pre_weight is always 0 without USE_PRE_WEIGHT)
+    printf("%6zu:w%6zu:pre%6zu:pst        ->[%4zu]\n", width(id), (size_t)0,
+           (size_t)pst_weight(id), (size_t)parent(id));
+  }
+};

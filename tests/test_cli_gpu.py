@@ -1,0 +1,96 @@
+"""The four CLIs end to end on the GPU, against the CPU checker and the published hep-th run."""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+PUB = json.load(open(os.path.join(GOLDEN, "hep_th_published.json")))
+BIN = os.path.join(ROOT, "sheep_amd", "bin")
+HEP = os.path.join(GOLDEN, "hep-th.dat")
+
+
+def run(*args):
+    return subprocess.run([os.path.join(BIN, args[0])] + list(args[1:]), capture_output=True,
+                          text=True, check=True).stdout
+
+
+def read_tre(path):
+    raw = np.fromfile(path, dtype=np.uint32)
+    body = raw[1:].reshape(-1, 2)[: int(raw[0])]
+    return body[:, 0].copy(), body[:, 1].copy()
+
+
+def test_graph2tree_faqs_and_timers(gpu, tmp_path):
+    out = run("graph2tree", HEP, "-f", "-c")
+    for line in ("Loaded graph in:", "Sorted in:", "Mapped in:", "Tree is valid."):
+        assert line in out
+    f = PUB["treefaqs"]
+    assert "TREEFAQS: width:%d\troots:%d" % (f["width"], f["roots"]) in out
+    assert "verts:%d\tedges:%d" % (f["verts"], f["edges"]) in out
+    assert "halo:%d\tcore:%d" % (f["halo"], f["core"]) in out
+
+
+def test_graph2tree_tre_equals_checker(gpu, oracle, hep_edges, tmp_path):
+    tre = str(tmp_path / "hep.tre")
+    run("graph2tree", HEP, "-o", tre)
+    assert os.path.getsize(tre) == 60884
+    p, s = read_tre(tre)
+    op, os_ = oracle.build_tree(hep_edges, oracle.degree_sequence(hep_edges))
+    assert np.array_equal(p, op) and np.array_equal(s, os_)
+
+
+def test_partition_tree_degree_sequence_from_gpu(gpu, tmp_path):
+    """partition_tree -g G - T k: the '-' sequence is degreeSequence on the GPU."""
+    tre = str(tmp_path / "hep.tre")
+    run("graph2tree", HEP, "-o", tre)
+    out = run("partition_tree", "-f", "-g", HEP, "-", tre, "2", "16", "32")
+    downs = [int(x) for x in re.findall(r"ECV\(down\): (\d+)", out)]
+    want = {r["k"]: r["ecv_down"] for r in PUB["partitions"]}
+    assert downs == [want[2], want[16], want[32]]
+
+
+def test_degree_sequence_file_mode(gpu, oracle, tmp_path):
+    sq = str(tmp_path / "hep.fseq")
+    out = run("degree_sequence", HEP, sq)
+    assert out.startswith("Sorted in: ")
+    got = np.array([int(x) for x in open(sq).read().split()], np.uint32)
+    assert np.array_equal(got, oracle.degree_sequence(oracle.read_dat_xs1reader(HEP), oracle.FILE))
+
+
+def test_partial_loads_and_merge_trees(gpu, oracle, hep_edges, tmp_path):
+    """graph2tree -l i/k -s SEQ partial trees, pairwise merge_trees == the serial tree
+    (README:112-121; scripts/map-worker.sh + reduce-worker.sh)."""
+    sq = str(tmp_path / "hep.seq")
+    seq = oracle.degree_sequence(hep_edges)
+    open(sq, "w").write("".join("%d\n" % x for x in seq))
+    k = 4
+    parts = []
+    for i in range(1, k + 1):
+        t = str(tmp_path / ("P%d.tre" % i))
+        run("graph2tree", HEP, "-l", "%d/%d" % (i, k), "-s", sq, "-o", t)
+        parts.append(t)
+    run("merge_trees", parts[0], parts[1], "-o", str(tmp_path / "A.tre"))
+    run("merge_trees", parts[2], parts[3], "-o", str(tmp_path / "B.tre"))
+    out = run("merge_trees", "-f", str(tmp_path / "A.tre"), str(tmp_path / "B.tre"), "-o",
+              str(tmp_path / "M.tre"))
+    p, s = read_tre(str(tmp_path / "M.tre"))
+    op, os_ = oracle.build_tree(hep_edges, seq)
+    assert np.array_equal(p, op) and np.array_equal(s, os_)
+    assert "halo:%d" % PUB["treefaqs"]["halo"] in out
+
+
+def test_graph2tree_partition_output(gpu, oracle, hep_edges, tmp_path):
+    """graph2tree -p K -o PREFIX: the fast partition path (graph2tree.cpp:203-216)."""
+    prefix = str(tmp_path / "hp")
+    run("graph2tree", HEP, "-p", "4", "-o", prefix)
+    seq = oracle.degree_sequence(hep_edges)
+    p, s = oracle.build_tree(hep_edges, seq)
+    parts = oracle.PartTree(p, s).partition(seq, 4)
+    n = sum(1 for q in range(4) for _ in open("%s%04d" % (prefix, q)))
+    assert n == len(hep_edges)
