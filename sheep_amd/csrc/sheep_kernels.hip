@@ -650,6 +650,10 @@ __device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t cbase = 0, cend = 0;  // wave-uniform chunk cursor
+  const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  uint64_t chunk_k = 0;
+  (void)next;
   bool active = false, exhausted = false;
   ZState s;
   ZCount c;
@@ -659,11 +663,11 @@ __device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
     uint64_t freem = __ballot(!active);
     while (freem && !exhausted) {
       if (cbase >= cend) {
-        unsigned long long st = 0;
-        if (lane == 0) st = atomicAdd(next, (unsigned long long)CH);
-        uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)st);
-        uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(st >> 32));
-        st = ((unsigned long long)hi32 << 32) | lo32;
+        // the wave's next chunk: static stride over the grid, so all waves sweep the edge
+        // list together in increasing order with no shared counter (a single global cursor
+        // serialises: one same-address atomic per chunk)
+        uint64_t st = (wave_id + chunk_k * nwaves) * (uint64_t)CH;
+        ++chunk_k;
         if (st >= n) { exhausted = true; break; }
         cbase = st;
         cend = st + CH < n ? st + CH : n;
@@ -703,14 +707,14 @@ __global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __
 // balanced lane queue, recording pre-bucket roots it links.
 template <bool STATS>
 __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
-                         const uint32_t* __restrict__ n_kept, uint32_t* parent, uint32_t* jump,
+                         uint64_t n, uint32_t* parent, uint32_t* jump,
                          unsigned long long* next, unsigned long long* stats, uint32_t B0,
                          uint32_t* linked, uint32_t* n_linked) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
-  tree_queue_body<0, 1, STATS, true>(kb, kg, *n_kept, parent, jump, next, stats, rec);
+  tree_queue_body<0, 1, STATS, true>(kb, kg, n, parent, jump, next, stats, rec);
 }
 
 typedef void (*TreeKernel)(const uint32_t*, const uint32_t*, uint64_t, uint32_t*, uint32_t*,
@@ -869,16 +873,13 @@ __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __rest
       rem &= ~same;
     }
     if (STATS) { edges += valid; kept += keep; }
-    uint64_t km = __ballot(keep);
-    uint32_t slot = 0;
-    if (lane == 0 && km) slot = atomicAdd(n_kept, (uint32_t)__popcll(km));
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    if (keep) {
-      uint32_t pos = slot + (uint32_t)__popcll(km & (lane ? (~0ull >> (64 - lane)) : 0ull));
-      kept_b[pos] = b;
-      kept_g[pos] = g;
+    // kept pairs stay in place (INVALID holes): no shared append cursor
+    if (valid) {
+      kept_b[idx - e_begin] = keep ? b : INV;
+      kept_g[idx - e_begin] = g;
     }
   }
+  (void)n_kept;
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
     atomicAdd(&stats[1], (unsigned long long)c.steps);
@@ -954,13 +955,13 @@ void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, 
       hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
                          uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<true>, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
-                         (const uint32_t*)kept_g, (const uint32_t*)n_kept, parent, jump, next, st + 8,
+                         (const uint32_t*)kept_g, e_end - e_begin, parent, jump, next, st + 8,
                          B0, linked, n_linked);
     } else {
       hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
                          uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<false>, dim3(MAX_GRID), dim3(BLOCK), 0, s,
-                         (const uint32_t*)kept_b, (const uint32_t*)kept_g, (const uint32_t*)n_kept,
+                         (const uint32_t*)kept_b, (const uint32_t*)kept_g, e_end - e_begin,
                          parent, jump, next, st + 8, B0, linked, n_linked);
     }
   } else {

@@ -1,0 +1,89 @@
+"""The sharded pipeline (sheep_amd.dist) on CPU with gloo: world_size 2 and 3, edge shards
+as graph2tree -l i/P, degree all-reduce, partial trees, log2 pairwise reduce to rank 0.
+The per-rank kernels are the CPU checker here (test-only backend); the orchestration and the
+collectives are the product code."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class CheckerOps:
+    """Test-only stand-in for the HIP kernels: the CPU checker on torch CPU tensors."""
+
+    def __init__(self, O):
+        self.O = O
+        self.seq = None
+
+    def degree(self, uv, n_ids, mode):
+        return torch.from_numpy(self.O.degree(uv.numpy(), mode, n_ids).astype(np.uint32))
+
+    def sequence(self, deg):
+        self.seq = self.O.sequence(deg.numpy().astype(np.uint32))
+        rmap = np.full(deg.numel(), 0xFFFFFFFF, np.uint32)
+        rmap[self.seq] = np.arange(len(self.seq), dtype=np.uint32)
+        return torch.from_numpy(self.seq.copy()), torch.from_numpy(rmap), len(self.seq)
+
+    def build_tree(self, uv, rmap, n_seq):
+        p, s = self.O.build_tree(uv.numpy(), self.seq)
+        return torch.from_numpy(p.copy()), torch.from_numpy(s.copy())
+
+    def merge_into(self, pa, sa, pb, sb, n):
+        p, s = self.O.merge(pa.numpy(), sa.numpy(), pb.numpy(), sb.numpy())
+        pa.copy_(torch.from_numpy(p))
+        sa.copy_(torch.from_numpy(s))
+
+
+def _worker(rank, world, port, scale, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from sheep_amd.dist import build_tree_sharded, shard_bounds
+
+        m = 16 << scale
+        lo, hi = shard_bounds(m, rank, world)
+        uv = torch.from_numpy(O.rmat(scale, 16, 3, lo, hi).astype(np.uint32))
+        seq, parent, pst, n = build_tree_sharded(uv, 1 << scale, CheckerOps(O))
+        if rank == 0:
+            result_q.put((seq.numpy().copy(), parent.numpy().copy(), pst.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_equals_serial(oracle, world):
+    scale = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(world, _free_port(), scale, q), nprocs=world, join=True,
+                       start_method="spawn")
+    seq, parent, pst = q.get(timeout=60)
+    uv = oracle.rmat(scale, 16, 3)
+    oseq = oracle.degree_sequence(uv)
+    p, s = oracle.build_tree(uv, oseq)
+    assert np.array_equal(seq, oseq)
+    assert np.array_equal(parent, p) and np.array_equal(pst, s)
+
+
+def test_shard_bounds_cover():
+    from sheep_amd.dist import shard_bounds
+
+    for m in (0, 1, 7, 1000):
+        for P in (1, 2, 3, 8):
+            b = [shard_bounds(m, r, P) for r in range(P)]
+            assert b[0][0] == 0 and b[-1][1] == m
+            assert all(b[i][1] == b[i + 1][0] for i in range(P - 1))
