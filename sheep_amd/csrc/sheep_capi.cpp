@@ -165,15 +165,12 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   if (d_rank) launch_fill(d_rank, INV, n_ids, s);
   if (n_seq == 0) return 0;
   int passes = (bits_for(maxdeg) + 7) / 8;
-  uint32_t* ka = (uint32_t*)c.scratch.get("seq_ka", (size_t)n_ids * 4);
-  uint32_t* va = (uint32_t*)c.scratch.get("seq_va", (size_t)n_ids * 4);
-  uint32_t* kb = (uint32_t*)c.scratch.get("seq_kb", (size_t)n_ids * 4);
-  uint32_t* vb = (uint32_t*)c.scratch.get("seq_vb", (size_t)n_ids * 4);
-  uint32_t* tmp = (uint32_t*)c.scratch.get("radix_tmp", radix_tmp_words(n_ids) * 4);
-  int which = radix_sort_pairs(d_deg, nullptr, ka, va, kb, vb, n_ids, 0, 8 * passes, tmp, s);
-  const uint32_t* sorted_ids = which == 0 ? va : vb;
-  HIP_CHECK(hipMemcpyAsync(d_seq, sorted_ids + zeros, (size_t)n_seq * 4, hipMemcpyDeviceToDevice, s));
-  if (d_rank) launch_rank_scatter(d_seq, n_seq, d_rank, c.d_err, s);
+  uint64_t* items = (uint64_t*)c.scratch.get("seq_items", (size_t)n_ids * 8);
+  uint64_t* items_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_ids * 8);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
+  launch_pack_deg(d_deg, n_ids, items, s);
+  uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
+  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s);
   return n_seq;
 }
 
@@ -186,12 +183,10 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n_seq * 4);
   launch_fill(jump, 0, n_seq, s);
   if (m == 0) return;
-  uint32_t* hi = (uint32_t*)c.scratch.get("e_hi", m * 4);
-  uint32_t* lo = (uint32_t*)c.scratch.get("e_lo", m * 4);
-  uint32_t* ka = (uint32_t*)c.scratch.get("e_ka", m * 4);
-  uint32_t* va = (uint32_t*)c.scratch.get("e_va", m * 4);
-  uint32_t* tmp = (uint32_t*)c.scratch.get("radix_tmp", radix_tmp_words(m) * 4);
-  launch_edge_pass(d_uv, m, d_rank, n_rank, d_pst, hi, lo, c.d_err, s);
+  uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
+  uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
+  launch_edge_pass(d_uv, m, d_rank, n_rank, d_pst, items, c.d_err, s);
   if (tm) tm->mark("edge_pass");
   const char* ea = getenv("SHEEP_TREE_ALGO");
   bool kb = !(ea && strcmp(ea, "zip") == 0);
@@ -201,15 +196,14 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   // kb needs edges fully sorted by hi (bucket ranges + wave dedupe); the plain zipper only
   // needs them bucketed by the top 16 bits (order affects work, never the result).
   int lo_bit = kb ? 0 : std::max(0, top - 16);
-  int which = radix_sort_pairs(hi, lo, ka, va, hi, lo, m, lo_bit, top, tmp, s);
-  const uint32_t* shi = which == 0 ? ka : hi;
-  const uint32_t* slo = which == 0 ? va : lo;
+  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top, tmp, s);
+  uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
   if (tm) tm->mark("bucket_sort");
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   if (!kb) {
     const char* ev = getenv("SHEEP_TREE_VARIANT");
     int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
-    launch_tree_insert(shi, slo, m, d_parent, jump, variant, stats, ws, s);
+    launch_tree_insert(sorted, m, d_parent, jump, variant, stats, ws, s);
   } else {
     const char* ek = getenv("SHEEP_KB_BUCKETS");
     uint32_t K = ek ? (uint32_t)atoi(ek) : 16;
@@ -217,15 +211,15 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
     uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
     uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 16);
-    // the sort's free ping-pong pair holds the kept (b, g) list of a bucket
-    uint32_t* kept_b = which == 0 ? hi : ka;
-    uint32_t* kept_g = which == 0 ? lo : va;
+    // the sort's free ping-pong buffer holds the kept (b, g) pairs of a bucket
+    uint32_t* kept_b = (uint32_t*)spare;
+    uint32_t* kept_g = (uint32_t*)spare + m;
     unsigned long long* bounds =
         (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
     launch_iota(uf, n_seq, s);
     launch_iota(label, n_seq, s);
     (void)hipMemsetAsync(ws, 0, 64 * 2, s);
-    launch_kb_bounds(shi, m, K, bounds, s);
+    launch_kb_bounds(sorted, m, K, bounds, s);
     std::vector<unsigned long long> hb(2 * (K + 1));
     HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -237,7 +231,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
       if (bk.empty() || (uint32_t)hb[2 * k] > bk.back().first) bk.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
     bk.emplace_back(n_seq, m_valid);
     for (size_t k = 0; k + 1 < bk.size(); ++k)
-      launch_kb_bucket(shi, slo, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
+      launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
                        label, d_parent, jump, kept_b, kept_g, linked, counters, stats, ws, s);
   }
   if (tm) tm->mark("tree_insert");

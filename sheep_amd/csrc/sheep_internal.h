@@ -49,26 +49,23 @@ void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max
 size_t scan_tmp_words(uint64_t n);
 void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp,
                            hipStream_t s);
-// Stable LSD radix sort of (key, val) pairs on bits [bit_lo, bit_hi) of key.  vals_in NULL
-// means val = index.  Buffers a/b ping-pong; returns which buffer (0 = a, 1 = b) holds the
-// result.  tmp needs radix_tmp_words(n) u32.
-size_t radix_tmp_words(uint64_t n);
-int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_a,
-                     uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, uint64_t n, int bit_lo,
-                     int bit_hi, uint32_t* tmp, hipStream_t s);
+size_t rsort_tmp_words(uint64_t n);
+uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
+                         int bit_hi, uint32_t* tmp, hipStream_t s);
+void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s);
+void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
+                       uint32_t* rank, hipStream_t s);
 void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s);
 void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
                          hipStream_t s);
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                      uint32_t* pst, uint32_t* hi_out, uint32_t* lo_out, uint32_t* err,
-                      hipStream_t s);
+                      uint32_t* pst, uint64_t* items, uint32_t* err, hipStream_t s);
 // variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
-void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
-                        uint32_t* jump, int variant, bool stats, unsigned long long* ws,
-                        hipStream_t s);
-void launch_kb_bounds(const uint32_t* hi, uint64_t n, uint32_t K, unsigned long long* out,
+void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
+                        int variant, bool stats, unsigned long long* ws, hipStream_t s);
+void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K, unsigned long long* out,
                       hipStream_t s);
-void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, uint64_t e_end,
+void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
                       uint32_t* counters, bool stats, unsigned long long* st, hipStream_t s);

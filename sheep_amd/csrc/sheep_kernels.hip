@@ -4,8 +4,9 @@
 // here is GEMM-shaped, so there is no MFMA.  Wave = 64 lanes throughout (ballots are 64-bit).
 //
 //   k_degree        per-vertex degree (sequence.h:101-107 / graph_wrapper.h:87-89)
-//   k_radix_*       stable LSD radix sort, LDS-ranked per 4096-key tile (degree sequence:
-//                   sequence.h:55-61; edge bucketing by max(rank))
+//   k_degb_*        LDS-bucketed degree histogram (large inputs)
+//   k_rsort_*       stable LSD radix sort of packed u64 items, LDS-ranked and LDS-staged
+//                   8192-item tiles (degree sequence: sequence.h:55-61; edges by max(rank))
 //   k_scan_*        exclusive scan (radix offsets)
 //   k_edge_pass     rank translation, pst_weight (jtree.cpp:84-87), (lo,hi) tree edges
 //   k_tree_insert   lock-free elimination-tree insertion ("zipper"), replacing the
@@ -356,43 +357,76 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
 }
 
 // ---------------------------------------------------------------------------------------
-// Stable LSD radix sort, 8-bit digits.  Pass = count (LDS histogram per tile, digit-major
-// counts matrix) -> exclusive scan -> scatter (per-chunk stable ranking by 64-lane ballot
-// match + per-wave digit counts in LDS).
+// Stable LSD radix sort of packed u64 items (key = upper 32 bits), 8-bit digits.
+// Tile = 1024 threads x 8 items.  Per pass: k_rsort_count (tile digit histograms, digit-major
+// matrix) -> exclusive scan -> k_rsort_scatter: the tile is ranked stably in LDS (64-lane
+// ballot match per chunk, per-wave digit counts), staged in LDS in digit order, and written
+// out so that consecutive lanes store consecutive addresses of one digit run.
 // ---------------------------------------------------------------------------------------
-__global__ void k_radix_count(const uint32_t* __restrict__ keys, uint64_t n, int shift,
-                              uint32_t* __restrict__ counts, uint32_t nblocks) {
+static constexpr int RS_THREADS = 1024;
+static constexpr int RS_ITEMS = 8;
+static constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
+static constexpr int RS_WAVES = RS_THREADS / 64;
+
+__global__ void __launch_bounds__(RS_THREADS)
+k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* __restrict__ counts,
+              uint32_t ntiles) {
   __shared__ uint32_t hist[256];
-  hist[threadIdx.x] = 0;
+  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * TILE;
-  for (int i = 0; i < ITEMS; ++i) {
-    uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
-    if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & 255u], 1u);
+  uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    uint64_t idx = base + (uint64_t)i * RS_THREADS + threadIdx.x;
+    if (idx < n) atomicAdd(&hist[(uint32_t)(in[idx] >> (32 + shift)) & 255u], 1u);
   }
   __syncthreads();
-  counts[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = hist[threadIdx.x];
+  if (threadIdx.x < 256) counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
 }
 
-__global__ void k_radix_scatter(const uint32_t* __restrict__ keys_in,
-                                const uint32_t* __restrict__ vals_in,
-                                uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                uint64_t n, int shift, const uint32_t* __restrict__ offsets,
-                                uint32_t nblocks) {
-  __shared__ uint32_t running[256];
-  __shared__ uint32_t whist[BLOCK / 64][256];
+__global__ void __launch_bounds__(RS_THREADS)
+k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n, int shift,
+                const uint32_t* __restrict__ offsets, uint32_t ntiles) {
+  __shared__ uint64_t stage[RS_TILE];
+  __shared__ uint32_t whist[RS_WAVES][256];
+  __shared__ uint32_t tstart[256], running[256], goff[256], wsum[RS_WAVES];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  running[t] = offsets[(uint64_t)t * nblocks + blockIdx.x];
-  for (int i = 0; i < BLOCK / 64; ++i) whist[i][t] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
+  uint64_t item[RS_ITEMS];
+  uint32_t dg[RS_ITEMS];
+  if (t < 256) { running[t] = 0; goff[t] = offsets[(uint64_t)t * ntiles + blockIdx.x]; }
+  for (int i = t; i < RS_WAVES * 256; i += RS_THREADS) (&whist[0][0])[i] = 0;
+#pragma unroll
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    uint32_t li = (uint32_t)i * RS_THREADS + t;
+    item[i] = li < tile_n ? in[base + li] : 0ull;
+    dg[i] = (uint32_t)(item[i] >> (32 + shift)) & 255u;
+  }
   __syncthreads();
-  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint64_t base = (uint64_t)blockIdx.x * TILE;
-  for (int c = 0; c < ITEMS; ++c) {
-    uint64_t idx = base + (uint64_t)c * BLOCK + t;
-    bool valid = idx < n;
-    uint32_t key = valid ? keys_in[idx] : 0u;
-    uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
-    uint32_t d = (key >> shift) & 255u;
+  // tile digit totals -> tstart (exclusive); reuse whist[0] as the histogram
+  for (int i = 0; i < RS_ITEMS; ++i)
+    if ((uint32_t)i * RS_THREADS + t < tile_n) atomicAdd(&whist[0][dg[i]], 1u);
+  __syncthreads();
+  if (t < 256) {
+    uint32_t v = whist[0][t];
+    uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = incl;
+    tstart[t] = incl - v;  // within-wave exclusive; waves 0..3 cover the 256 digits
+  }
+  __syncthreads();
+  if (t < 256) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    tstart[t] += add;
+    whist[0][t] = 0;
+  }
+  __syncthreads();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int c = 0; c < RS_ITEMS; ++c) {
+    bool valid = (uint32_t)c * RS_THREADS + t < tile_n;
+    uint32_t d = dg[c];
     uint64_t match = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -404,48 +438,78 @@ __global__ void k_radix_scatter(const uint32_t* __restrict__ keys_in,
     if (valid && before == 0) whist[w][d] = (uint32_t)__popcll(match);
     __syncthreads();
     if (valid) {
-      uint32_t pos = running[d] + before;
+      uint32_t pos = tstart[d] + running[d] + before;
       for (int i = 0; i < w; ++i) pos += whist[i][d];
-      keys_out[pos] = key;
-      vals_out[pos] = val;
+      stage[pos] = item[c];
     }
     __syncthreads();
-    uint32_t tot = 0;
-    for (int i = 0; i < BLOCK / 64; ++i) { tot += whist[i][t]; whist[i][t] = 0; }
-    running[t] += tot;
+    if (t < 256) {
+      uint32_t tot = 0;
+      for (int i = 0; i < RS_WAVES; ++i) { tot += whist[i][t]; whist[i][t] = 0; }
+      running[t] += tot;
+    }
     __syncthreads();
+  }
+  for (uint32_t j = t; j < tile_n; j += RS_THREADS) {
+    uint64_t it = stage[j];
+    uint32_t d = (uint32_t)(it >> (32 + shift)) & 255u;
+    out[(uint64_t)goff[d] + (j - tstart[d])] = it;
   }
 }
 
-size_t radix_tmp_words(uint64_t n) {
-  uint64_t nb = (n + TILE - 1) / TILE;
-  return 256 * nb + scan_tmp_words(256 * nb);
+size_t rsort_tmp_words(uint64_t n) {
+  uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
+  return 256 * nt + scan_tmp_words(256 * nt);
 }
 
-int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_a,
-                     uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, uint64_t n, int bit_lo,
-                     int bit_hi, uint32_t* tmp, hipStream_t s) {
-  uint64_t nb = (n + TILE - 1) / TILE;
+// Sorts n items on bits [bit_lo, bit_hi) of their upper word; returns the buffer holding the
+// result (in, a or b).  `in` is never written.
+uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
+                         int bit_hi, uint32_t* tmp, hipStream_t s) {
+  uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
-  uint32_t* stmp = tmp + 256 * nb;
-  const uint32_t* kin = keys_in;
-  const uint32_t* vin = vals_in;
-  int cur = -1;
+  uint32_t* stmp = tmp + 256 * nt;
+  const uint64_t* src = in;
+  uint64_t* dst = a;
   for (int shift = bit_lo; shift < bit_hi; shift += 8) {
-    uint32_t* kout = (cur == 0) ? keys_b : keys_a;
-    uint32_t* vout = (cur == 0) ? vals_b : vals_a;
     if (n) {
-      hipLaunchKernelGGL(k_radix_count, dim3((unsigned)nb), dim3(BLOCK), 0, s, kin, n, shift,
-                         counts, (uint32_t)nb);
-      launch_scan_exclusive(counts, counts, 256 * nb, stmp, s);
-      hipLaunchKernelGGL(k_radix_scatter, dim3((unsigned)nb), dim3(BLOCK), 0, s, kin, vin, kout,
-                         vout, n, shift, (const uint32_t*)counts, (uint32_t)nb);
+      hipLaunchKernelGGL(k_rsort_count, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n, shift,
+                         counts, (uint32_t)nt);
+      launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
+      hipLaunchKernelGGL(k_rsort_scatter, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst, n,
+                         shift, (const uint32_t*)counts, (uint32_t)nt);
     }
-    cur = (cur == 0) ? 1 : 0;
-    kin = kout;
-    vin = vout;
+    src = dst;
+    dst = (dst == a) ? b : a;
   }
-  return cur;
+  return (uint64_t*)src;
+}
+
+// Degree sequence helpers: items = (deg << 32 | id); after the sort, seq = ids past the
+// zero-degree prefix and rank[seq[i]] = i (jtree.h:165-168) in the same pass.
+__global__ void k_pack_deg(const uint32_t* __restrict__ deg, uint32_t n, uint64_t* __restrict__ items) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    items[i] = ((uint64_t)deg[i] << 32) | i;
+}
+
+__global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros, uint32_t n_seq,
+                             uint32_t* __restrict__ seq, uint32_t* __restrict__ rank) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_seq; i += gridDim.x * blockDim.x) {
+    uint32_t v = (uint32_t)items[zeros + i];
+    seq[i] = v;
+    if (rank) rank[v] = i;
+  }
+}
+
+void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_pack_deg, dim3(grid_for(n)), dim3(BLOCK), 0, s, deg, n, items);
+}
+
+void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
+                       uint32_t* rank, hipStream_t s) {
+  if (n_seq)
+    hipLaunchKernelGGL(k_unpack_seq, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, items, zeros, n_seq,
+                       seq, rank);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -476,8 +540,7 @@ void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, ui
 // ---------------------------------------------------------------------------------------
 __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
                             const uint32_t* __restrict__ rank, uint32_t n_rank,
-                            uint32_t* __restrict__ pst, uint32_t* __restrict__ hi_out,
-                            uint32_t* __restrict__ lo_out, uint32_t* err) {
+                            uint32_t* __restrict__ pst, uint64_t* __restrict__ items, uint32_t* err) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint2 e = uv[i];
@@ -494,17 +557,15 @@ __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
         if (lo != INV) atomicAdd(&pst[lo], 1u);
       }
     }
-    hi_out[i] = hi;
-    lo_out[i] = lo;
+    items[i] = ((uint64_t)hi << 32) | lo;
   }
 }
 
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                      uint32_t* pst, uint32_t* hi_out, uint32_t* lo_out, uint32_t* err,
-                      hipStream_t s) {
+                      uint32_t* pst, uint64_t* items, uint32_t* err, hipStream_t s) {
   if (m == 0) return;
   hipLaunchKernelGGL(k_edge_pass, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, rank,
-                     n_rank, pst, hi_out, lo_out, err);
+                     n_rank, pst, items, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -617,18 +678,18 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, uint64_t 
 
 // Variant A: one edge per thread per iteration, grid-stride (a wave waits for its slowest lane).
 template <int LOAD, int JUMP, bool STATS>
-__global__ void k_tree_loop(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
-                            uint64_t n, uint32_t* parent, uint32_t* jump,
-                            unsigned long long* next, unsigned long long* stats) {
+__global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
+                            uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
   ZCount c;
   uint64_t edges = 0;
   uint32_t maxsteps = 0;
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint32_t b = hi[i];
+    uint64_t it = items[i];
+    uint32_t b = (uint32_t)(it >> 32);
     if (b == INV) continue;
     ZState s;
-    zstart(s, lo[i], b);
+    zstart(s, (uint32_t)it, b);
     uint32_t st0 = c.steps;
     while (!zip_step<LOAD, JUMP, STATS>(parent, jump, s, c)) {
     }
@@ -640,9 +701,19 @@ __global__ void k_tree_loop(const uint32_t* __restrict__ hi, const uint32_t* __r
 // Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order from
 // one global counter (one atomic per 512 edges) and every lane that finishes an edge takes
 // the next one at the following step, so a wave never idles behind its slowest lane.
+// Edge source of the queue: packed u64 items (hi << 32 | lo) or two u32 arrays.
+struct EdgeSrc {
+  const uint64_t* items;
+  const uint32_t* hi;
+  const uint32_t* lo;
+  __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a) const {
+    if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; }
+    else { b = hi[i]; a = (b != INV) ? lo[i] : 0u; }
+  }
+};
+
 template <int LOAD, int JUMP, bool STATS, bool REC>
-__device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
-                                                const uint32_t* __restrict__ lo, uint64_t n,
+__device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
                                                 uint32_t* parent, uint32_t* jump,
                                                 unsigned long long* next, unsigned long long* stats,
                                                 const ZRec& rec) {
@@ -677,9 +748,10 @@ __device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
       uint64_t avail = cend - cbase;
       if (!active && k < avail) {
         uint64_t idx = cbase + k;
-        uint32_t b = hi[idx];
+        uint32_t b, a;
+        src.get(idx, b, a);
         if (b != INV) {
-          zstart(s, lo[idx], b);
+          zstart(s, a, b);
           active = true;
           if (STATS) { edges++; st0 = c.steps; }
         }
@@ -697,10 +769,10 @@ __device__ __forceinline__ void tree_queue_body(const uint32_t* __restrict__ hi,
 }
 
 template <int LOAD, int JUMP, bool STATS>
-__global__ void k_tree_queue(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
-                             uint64_t n, uint32_t* parent, uint32_t* jump,
-                             unsigned long long* next, unsigned long long* stats) {
-  tree_queue_body<LOAD, JUMP, STATS, false>(hi, lo, n, parent, jump, next, stats, ZRec());
+__global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
+                             uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
+  EdgeSrc src{items, nullptr, nullptr};
+  tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, next, stats, ZRec());
 }
 
 // The kb in-bucket pass: the kept (g, b) list of a bucket (count on the device) through the
@@ -714,11 +786,12 @@ __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __rest
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
-  tree_queue_body<0, 1, STATS, true>(kb, kg, n, parent, jump, next, stats, rec);
+  EdgeSrc src{nullptr, kb, kg};
+  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
 }
 
-typedef void (*TreeKernel)(const uint32_t*, const uint32_t*, uint64_t, uint32_t*, uint32_t*,
-                           unsigned long long*, unsigned long long*);
+typedef void (*TreeKernel)(const uint64_t*, uint64_t, uint32_t*, uint32_t*, unsigned long long*,
+                           unsigned long long*);
 
 template <int LOAD, int JUMP, bool STATS>
 static TreeKernel pick_tree(int queue) {
@@ -733,15 +806,14 @@ static TreeKernel pick_tree(int load, int jmp, int queue) {
 }
 
 // variant = load + 4 * jump + 8 * queue; ws = 8 u64 words of device scratch (counter + stats).
-void launch_tree_insert(const uint32_t* hi, const uint32_t* lo, uint64_t n, uint32_t* parent,
-                        uint32_t* jump, int variant, bool stats, unsigned long long* ws,
-                        hipStream_t s) {
+void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
+                        int variant, bool stats, unsigned long long* ws, hipStream_t s) {
   if (n == 0) return;
   int load = variant & 3, jmp = (variant >> 2) & 1, queue = (variant >> 3) & 1;
   TreeKernel k = stats ? pick_tree<true>(load, jmp, queue) : pick_tree<false>(load, jmp, queue);
   (void)hipMemsetAsync(ws, 0, 8 * sizeof(unsigned long long), s);
   unsigned grid = queue ? (unsigned)MAX_GRID : grid_for(n);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, hi, lo, n, parent, jump, ws, ws + 1);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, items, n, parent, jump, ws, ws + 1);
 }
 
 __device__ void zip_insert(uint32_t* parent, uint32_t* jump, uint32_t a, uint32_t b) {
@@ -845,8 +917,7 @@ __device__ __forceinline__ void zip_insert_rec(uint32_t* parent, uint32_t* jump,
 }
 
 template <bool STATS>
-__global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
-                         uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
+__global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
                          const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
                          uint32_t* n_kept, unsigned long long* stats, int mapmode) {
   const int lane = threadIdx.x & 63;
@@ -857,8 +928,9 @@ __global__ void k_kb_map(const uint32_t* __restrict__ hi, const uint32_t* __rest
   for (uint64_t base = e_begin + wave * 64; base < e_end; base += nwaves * 64) {
     uint64_t idx = base + lane;
     bool valid = idx < e_end;
-    uint32_t b = valid ? hi[idx] : INV;
-    uint32_t a = valid ? lo[idx] : 0;
+    uint64_t it = valid ? items[idx] : ~0ull;
+    uint32_t b = (uint32_t)(it >> 32);
+    uint32_t a = valid ? (uint32_t)it : 0u;
     uint32_t g = a;
     if (valid && a < B0 && mapmode != 2) g = label[uf_find<false>(uf, a)];
     // keep the first lane of every distinct (g, b) in the wave
@@ -911,33 +983,33 @@ __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, ui
 
 // Bucket boundaries by edge count: thread k finds m_valid (first INVALID hi), takes the rank at
 // position k*m_valid/K and lower_bounds it.  out[2k] = B_k, out[2k+1] = first edge of bucket k.
-__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t n, uint32_t key) {
+__device__ __forceinline__ uint64_t lower_bound_hi(const uint64_t* a, uint64_t n, uint32_t key) {
   uint64_t lo = 0, hi = n;
   while (lo < hi) {
     uint64_t mid = (lo + hi) >> 1;
-    if (a[mid] < key) lo = mid + 1; else hi = mid;
+    if ((uint32_t)(a[mid] >> 32) < key) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
 
-__global__ void k_kb_bounds(const uint32_t* __restrict__ hi, uint64_t n, uint32_t K,
+__global__ void k_kb_bounds(const uint64_t* __restrict__ items, uint64_t n, uint32_t K,
                             unsigned long long* out) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k > K) return;
-  uint64_t mv = lower_bound_u32(hi, n, INV);
+  uint64_t mv = lower_bound_hi(items, n, INV);
   if (k == K) { out[2 * K] = INV; out[2 * K + 1] = mv; return; }
   uint64_t pos = mv * k / K;
-  uint32_t B = (k == 0 || mv == 0) ? 0u : hi[pos];
+  uint32_t B = (k == 0 || mv == 0) ? 0u : (uint32_t)(items[pos] >> 32);
   out[2 * k] = B;
-  out[2 * k + 1] = lower_bound_u32(hi, mv, B);
+  out[2 * k + 1] = lower_bound_hi(items, mv, B);
 }
 
-void launch_kb_bounds(const uint32_t* hi, uint64_t n, uint32_t K, unsigned long long* out,
+void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K, unsigned long long* out,
                       hipStream_t s) {
-  hipLaunchKernelGGL(k_kb_bounds, dim3((K + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, hi, n, K, out);
+  hipLaunchKernelGGL(k_kb_bounds, dim3((K + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, items, n, K, out);
 }
 
-void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, uint64_t e_end,
+void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
                       uint32_t* counters, bool stats, unsigned long long* st, hipStream_t s) {
@@ -952,13 +1024,13 @@ void launch_kb_bucket(const uint32_t* hi, const uint32_t* lo, uint64_t e_begin, 
     unsigned grid = grid_for(waves * 64);
     (void)hipMemsetAsync(counters, 0, 16, s);
     if (stats) {
-      hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
+      hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0,
                          uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<true>, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
                          (const uint32_t*)kept_g, e_end - e_begin, parent, jump, next, st + 8,
                          B0, linked, n_linked);
     } else {
-      hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, hi, lo, e_begin, e_end, B0,
+      hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0,
                          uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
       hipLaunchKernelGGL(k_kb_zip<false>, dim3(MAX_GRID), dim3(BLOCK), 0, s,
                          (const uint32_t*)kept_b, (const uint32_t*)kept_g, e_end - e_begin,
