@@ -703,12 +703,14 @@ __global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint
 // the next one at the following step, so a wave never idles behind its slowest lane.
 // Edge source of the queue: packed u64 items (hi << 32 | lo) or two u32 arrays.
 struct EdgeSrc {
-  const uint64_t* items;
-  const uint32_t* hi;
+  const uint64_t* items;  // packed (hi << 32 | lo)
+  const uint32_t* hi;     // or hi[] / lo[]
   const uint32_t* lo;
+  uint32_t base = 0;      // or (items == hi == nullptr): b = base + i, a = lo[i]
   __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a) const {
     if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; }
-    else { b = hi[i]; a = (b != INV) ? lo[i] : 0u; }
+    else if (hi) { b = hi[i]; a = (b != INV) ? lo[i] : 0u; }
+    else { a = lo[i]; b = (a != INV) ? base + (uint32_t)i : INV; }
   }
 };
 
@@ -779,14 +781,14 @@ __global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uin
 // balanced lane queue, recording pre-bucket roots it links.
 template <bool STATS>
 __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
-                         uint64_t n, uint32_t* parent, uint32_t* jump,
+                         uint32_t kbase, uint64_t n, uint32_t* parent, uint32_t* jump,
                          unsigned long long* next, unsigned long long* stats, uint32_t B0,
                          uint32_t* linked, uint32_t* n_linked) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
-  EdgeSrc src{nullptr, kb, kg};
+  EdgeSrc src{nullptr, kb, kg, kbase};
   tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
 }
 
@@ -917,9 +919,13 @@ __device__ __forceinline__ void zip_insert_rec(uint32_t* parent, uint32_t* jump,
 }
 
 template <bool STATS>
-__global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0, uint32_t* uf,
+__global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
+                         uint64_t e_end, uint32_t B0, uint32_t* uf,
                          const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
-                         uint32_t* n_kept, unsigned long long* stats, int mapmode) {
+                         uint32_t* bitmap, unsigned long long* stats, int mapmode) {
+  // G: the component of the last pre-bucket vertex (in a degree-ordered sequence: the giant).
+  // Its (G, b) pairs go to a rank bitmap and become path edges (k_kb_path), not zipper walks.
+  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find<false>(uf, B0 - 1)] : INV;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -945,13 +951,14 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, u
       rem &= ~same;
     }
     if (STATS) { edges += valid; kept += keep; }
+    bool giant = keep && g == G;
+    if (giant) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
     // kept pairs stay in place (INVALID holes): no shared append cursor
     if (valid) {
-      kept_b[idx - e_begin] = keep ? b : INV;
+      kept_b[idx - e_begin] = (keep && !giant) ? b : INV;
       kept_g[idx - e_begin] = g;
     }
   }
-  (void)n_kept;
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
     atomicAdd(&stats[1], (unsigned long long)c.steps);
@@ -959,6 +966,43 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, u
     atomicAdd(&stats[3], (unsigned long long)c.fail);
     atomicAdd(&stats[5], (unsigned long long)kept);
   }
+}
+
+// Star -> path for the giant: G is adjacent to the marked ranks b1 < b2 < ... of the bucket.
+// For the etree that star is equivalent to the path G-b1-b2-...: at any threshold both
+// connect G with exactly the marked ranks present.  So each marked b gets the edge
+// (previous marked rank, b); if none is found within 64 words back, (G, b) — always valid,
+// only a longer walk.  pa[b] = the lower endpoint (INVALID for unmarked ranks).
+__device__ __forceinline__ void kb_path_body(uint32_t* __restrict__ bitmap, uint32_t B0,
+                                             uint32_t B1, uint32_t G, uint32_t* __restrict__ pa) {
+  const uint32_t w0 = B0 >> 5, w1 = (B1 + 31) >> 5;
+  for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += gridDim.x * blockDim.x) {
+    uint32_t bits = bitmap[w];
+    uint32_t lo_mask = (w == w0) ? (~0u << (B0 & 31)) : ~0u;
+    uint32_t hi_mask = (w == w1 - 1 && (B1 & 31)) ? ((1u << (B1 & 31)) - 1u) : ~0u;
+    bits &= lo_mask & hi_mask;
+    if (!bits) continue;
+    uint32_t pred = G;  // predecessor of this word's first marked rank
+    for (uint32_t v = w, k = 0; v > w0 && k < 64; --v, ++k) {
+      uint32_t pb = bitmap[v - 1] & ((v - 1 == w0) ? (~0u << (B0 & 31)) : ~0u);
+      if (pb) { pred = ((v - 1) << 5) + 31 - __clz(pb); break; }
+    }
+    for (uint32_t rem = bits; rem;) {
+      uint32_t b = (w << 5) + (__ffs(rem) - 1);
+      rem &= rem - 1;
+      pa[b] = pred;
+      pred = b;
+    }
+  }
+}
+
+__global__ void k_kb_giant(uint32_t* uf, const uint32_t* __restrict__ label, uint32_t B0, uint32_t* G) {
+  if (threadIdx.x == 0) *G = label[uf_find<false>(uf, B0 - 1)];
+}
+
+__global__ void k_kb_path(uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
+                          const uint32_t* __restrict__ G, uint32_t* __restrict__ pa) {
+  kb_path_body(bitmap, B0, B1, *G, pa);
 }
 
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
@@ -1012,32 +1056,35 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K, unsigned lo
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* counters, bool stats, unsigned long long* st, hipStream_t s) {
+                      uint32_t* bitmap, uint32_t* pa, uint32_t* counters, bool stats,
+                      unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
   int mapmode = em ? atoi(em) : 0;
-  // counters: [0] n_kept, [1] n_linked, [2..3] u64 queue cursor
-  uint32_t* n_kept = counters;
+  // counters: [1] n_linked, [3] G for the path kernel, [4..5] unused u64
   uint32_t* n_linked = counters + 1;
-  unsigned long long* next = (unsigned long long*)(counters + 2);
+  unsigned long long* next = (unsigned long long*)(counters + 4);
+  (void)hipMemsetAsync(counters, 0, 16, s);
+  auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
   if (e_end > e_begin) {
     uint64_t waves = (e_end - e_begin + 63) / 64;
     unsigned grid = grid_for(waves * 64);
-    (void)hipMemsetAsync(counters, 0, 16, s);
-    if (stats) {
-      hipLaunchKernelGGL(k_kb_map<true>, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
-      hipLaunchKernelGGL(k_kb_zip<true>, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
-                         (const uint32_t*)kept_g, e_end - e_begin, parent, jump, next, st + 8,
-                         B0, linked, n_linked);
-    } else {
-      hipLaunchKernelGGL(k_kb_map<false>, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0,
-                         uf, (const uint32_t*)label, kept_b, kept_g, n_kept, st, mapmode);
-      hipLaunchKernelGGL(k_kb_zip<false>, dim3(MAX_GRID), dim3(BLOCK), 0, s,
-                         (const uint32_t*)kept_b, (const uint32_t*)kept_g, e_end - e_begin,
-                         parent, jump, next, st + 8, B0, linked, n_linked);
+    auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
+    hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
+                       (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
+    if (B0 > 0 && mapmode == 0) {
+      hipLaunchKernelGGL(k_kb_giant, dim3(1), dim3(64), 0, s, uf, (const uint32_t*)label, B0,
+                         counters + 3);
+      hipLaunchKernelGGL(k_kb_path, dim3(grid_for(((B1 - B0) >> 5) + 2)), dim3(BLOCK), 0, s,
+                         bitmap, B0, B1, (const uint32_t*)(counters + 3), pa);
+      hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)nullptr,
+                         (const uint32_t*)(pa + B0), B0, (uint64_t)(B1 - B0), parent, jump, next,
+                         st + 8, B0, linked, n_linked);
+      (void)hipMemsetAsync(bitmap + (B0 >> 5), 0, (size_t)(((B1 + 31) >> 5) - (B0 >> 5)) * 4, s);
+      (void)hipMemsetAsync(pa + B0, 0xFF, (size_t)(B1 - B0) * 4, s);
     }
-  } else {
-    (void)hipMemsetAsync(counters, 0, 16, s);
+    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
+                       (const uint32_t*)kept_g, 0u, e_end - e_begin, parent, jump, next, st + 8,
+                       B0, linked, n_linked);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
