@@ -191,7 +191,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const char* ea = getenv("SHEEP_TREE_ALGO");
   bool kb = !(ea && strcmp(ea, "zip") == 0);
   const char* es = getenv("SHEEP_TREE_STATS");
-  bool stats = es && es[0] == '1';
+  bool stats = es && (es[0] == '1' || es[0] == '2');
   int top = bits_for(n_seq);
   // kb needs edges fully sorted by hi (bucket ranges + wave dedupe); the plain zipper only
   // needs them bucketed by the top 16 bits (order affects work, never the result).
@@ -234,10 +234,20 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     for (uint32_t k = 0; k < K; ++k)
       if (bk.empty() || (uint32_t)hb[2 * k] > bk.back().first) bk.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
     bk.emplace_back(n_seq, m_valid);
-    for (size_t k = 0; k + 1 < bk.size(); ++k)
+    bool per_bucket = es && es[0] == '2';
+    for (size_t k = 0; k + 1 < bk.size(); ++k) {
+      if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
       launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
                        label, d_parent, jump, kept_b, kept_g, linked, bitmap, pa, counters, stats,
                        ws, s);
+      if (per_bucket) {
+        unsigned long long h[16];
+        HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
+                k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[8], h[9], h[10], h[11], h[12]);
+      }
+    }
   }
   if (tm) tm->mark("tree_insert");
   if (stats) {

@@ -925,12 +925,12 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
                          uint32_t* bitmap, unsigned long long* stats, int mapmode) {
   // G: the component of the last pre-bucket vertex (in a degree-ordered sequence: the giant).
   // Its (G, b) pairs go to a rank bitmap and become path edges (k_kb_path), not zipper walks.
-  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find<false>(uf, B0 - 1)] : INV;
+  const uint32_t G = (B0 > 0 && mapmode == 4) ? label[uf_find<false>(uf, B0 - 1)] : INV;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   ZCount c;
-  uint64_t edges = 0, kept = 0;
+  uint64_t edges = 0, kept = 0, inb = 0;
   for (uint64_t base = e_begin + wave * 64; base < e_end; base += nwaves * 64) {
     uint64_t idx = base + lane;
     bool valid = idx < e_end;
@@ -950,7 +950,7 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
       if (lane != leader && ((same >> lane) & 1)) keep = false;
       rem &= ~same;
     }
-    if (STATS) { edges += valid; kept += keep; }
+    if (STATS) { edges += valid; kept += keep; inb += keep && a >= B0; }
     bool giant = keep && g == G;
     if (giant) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
     // kept pairs stay in place (INVALID holes): no shared append cursor
@@ -965,6 +965,7 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
     atomicAdd(&stats[2], (unsigned long long)c.cas);
     atomicAdd(&stats[3], (unsigned long long)c.fail);
     atomicAdd(&stats[5], (unsigned long long)kept);
+    atomicAdd(&stats[6], (unsigned long long)inb);
   }
 }
 
@@ -1071,7 +1072,7 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
     auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
     hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
                        (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
-    if (B0 > 0 && mapmode == 0) {
+    if (B0 > 0 && mapmode == 4) {
       hipLaunchKernelGGL(k_kb_giant, dim3(1), dim3(64), 0, s, uf, (const uint32_t*)label, B0,
                          counters + 3);
       hipLaunchKernelGGL(k_kb_path, dim3(grid_for(((B1 - B0) >> 5) + 2)), dim3(BLOCK), 0, s,
