@@ -41,7 +41,7 @@ for v in args.variants.split(","):
         ref = (parent.clone(), pst.clone())
     else:
         same = bool(torch.equal(parent, ref[0]) and torch.equal(pst, ref[1]))
-    os.environ["SHEEP_TREE_STATS"] = "1"
+    os.environ["SHEEP_TREE_STATS"] = os.environ.get("LAB_STATS", "1")
     device.build_tree(uv, rank, n_seq)
     torch.cuda.synchronize()
     print("variant %s tree_insert %.2f ms  other %s  same=%s" % (
