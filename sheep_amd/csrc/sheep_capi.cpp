@@ -206,7 +206,10 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_tree_insert(sorted, m, d_parent, jump, variant, stats, ws, s);
   } else {
     const char* ek = getenv("SHEEP_KB_BUCKETS");
-    uint32_t K = ek ? (uint32_t)atoi(ek) : 64;
+    const char* er = getenv("SHEEP_KB_RANKB");
+    uint32_t K_e = ek ? (uint32_t)atoi(ek) : 32;
+    uint32_t K_r = er ? (uint32_t)atoi(er) : 32;
+    uint32_t K = K_e + K_r;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
     uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
@@ -223,16 +226,20 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_iota(uf, n_seq, s);
     launch_iota(label, n_seq, s);
     (void)hipMemsetAsync(ws, 0, 64 * 2, s);
-    launch_kb_bounds(sorted, m, K, bounds, s);
+    launch_kb_bounds(sorted, m, K_e, K_r, n_seq, bounds, s);
     std::vector<unsigned long long> hb(2 * (K + 1));
     HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (tm) tm->mark("kb_bounds");
     uint64_t m_valid = hb[2 * K + 1];
     // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
+    std::vector<std::pair<uint32_t, uint64_t>> cand;
+    for (uint32_t k = 0; k < K; ++k) cand.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
+    std::sort(cand.begin(), cand.end());
     std::vector<std::pair<uint32_t, uint64_t>> bk;
-    for (uint32_t k = 0; k < K; ++k)
-      if (bk.empty() || (uint32_t)hb[2 * k] > bk.back().first) bk.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
+    for (auto& cb : cand)
+      if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
+    if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
     bk.emplace_back(n_seq, m_valid);
     bool per_bucket = es && es[0] == '2';
     for (size_t k = 0; k + 1 < bk.size(); ++k) {

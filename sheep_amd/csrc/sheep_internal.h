@@ -63,8 +63,8 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 // variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
 void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
                         int variant, bool stats, unsigned long long* ws, hipStream_t s);
-void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K, unsigned long long* out,
-                      hipStream_t s);
+void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
+                      uint32_t n_seq, unsigned long long* out, hipStream_t s);
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,

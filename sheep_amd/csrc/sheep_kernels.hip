@@ -1037,21 +1037,32 @@ __device__ __forceinline__ uint64_t lower_bound_hi(const uint64_t* a, uint64_t n
   return lo;
 }
 
-__global__ void k_kb_bounds(const uint64_t* __restrict__ items, uint64_t n, uint32_t K,
-                            unsigned long long* out) {
+// Bucket boundaries: K_e by edge count (rank at edge quantile k/K_e) and K_r by rank
+// (n_seq * k / K_r), so that no bucket is heavy in edges or wide in ranks (a wide bucket gets
+// no union-find help: its in-bucket walks are long).  out[2i] = rank B, out[2i+1] = first
+// edge with hi >= B; entry K_e + K_r carries (INVALID, m_valid).  The host merges and sorts.
+__global__ void k_kb_bounds(const uint64_t* __restrict__ items, uint64_t n, uint32_t K_e,
+                            uint32_t K_r, uint32_t n_seq, unsigned long long* out) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t K = K_e + K_r;
   if (k > K) return;
   uint64_t mv = lower_bound_hi(items, n, INV);
   if (k == K) { out[2 * K] = INV; out[2 * K + 1] = mv; return; }
-  uint64_t pos = mv * k / K;
-  uint32_t B = (k == 0 || mv == 0) ? 0u : (uint32_t)(items[pos] >> 32);
+  uint32_t B;
+  if (k < K_e) {
+    uint64_t pos = mv * k / K_e;
+    B = (k == 0 || mv == 0) ? 0u : (uint32_t)(items[pos] >> 32);
+  } else {
+    B = (uint32_t)((uint64_t)n_seq * (k - K_e) / K_r);
+  }
   out[2 * k] = B;
   out[2 * k + 1] = lower_bound_hi(items, mv, B);
 }
 
-void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K, unsigned long long* out,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(k_kb_bounds, dim3((K + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, items, n, K, out);
+void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
+                      uint32_t n_seq, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_kb_bounds, dim3((K_e + K_r + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s,
+                     items, n, K_e, K_r, n_seq, out);
 }
 
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
