@@ -207,8 +207,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   } else {
     const char* ek = getenv("SHEEP_KB_BUCKETS");
     const char* er = getenv("SHEEP_KB_RANKB");
-    uint32_t K_e = ek ? (uint32_t)atoi(ek) : 32;
-    uint32_t K_r = er ? (uint32_t)atoi(er) : 32;
+    uint32_t K_e = ek ? (uint32_t)atoi(ek) : 64;
+    uint32_t K_r = er ? (uint32_t)atoi(er) : 0;
     uint32_t K = K_e + K_r;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);

@@ -540,21 +540,22 @@ void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, ui
 // ---------------------------------------------------------------------------------------
 __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
                             const uint32_t* __restrict__ rank, uint32_t n_rank,
-                            uint32_t* __restrict__ pst, uint64_t* __restrict__ items, uint32_t* err) {
+                            uint32_t* __restrict__ pst, uint64_t* __restrict__ items, uint32_t* err,
+                            int ablate) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint2 e = uv[i];
     uint32_t hi = INV, lo = INV;
     if (e.x != e.y) {
       bool ox = e.x >= n_rank, oy = e.y >= n_rank;
-      uint32_t rx = ox ? INV : rank[e.x];
-      uint32_t ry = oy ? INV : rank[e.y];
+      uint32_t rx = ox ? INV : ((ablate & 2) ? e.x : rank[e.x]);
+      uint32_t ry = oy ? INV : ((ablate & 2) ? e.y : rank[e.y]);
       if ((ox && ry != INV) || (oy && rx != INV)) {
         atomicOr(err, ERR_RANGE);
       } else {
         lo = min(rx, ry);
         hi = max(rx, ry);
-        if (lo != INV) atomicAdd(&pst[lo], 1u);
+        if (lo != INV && !(ablate & 1)) atomicAdd(&pst[lo], 1u);
       }
     }
     items[i] = ((uint64_t)hi << 32) | lo;
@@ -564,8 +565,9 @@ __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                       uint32_t* pst, uint64_t* items, uint32_t* err, hipStream_t s) {
   if (m == 0) return;
+  const char* ea = getenv("SHEEP_EP_ABLATE");  // diagnostics only: 1 = no pst, 2 = no gathers
   hipLaunchKernelGGL(k_edge_pass, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, rank,
-                     n_rank, pst, items, err);
+                     n_rank, pst, items, err, ea ? atoi(ea) : 0);
 }
 
 // ---------------------------------------------------------------------------------------
