@@ -85,6 +85,12 @@ int sheep_merge_trees(const uint32_t* parent_a, const uint32_t* pst_a, const uin
 int sheep_degree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
                      uint32_t* d_deg, void* stream);
 
+/* As sheep_degree_dev, and d_selfc (nullable, n_ids entries) receives the number of
+ * self-loop records at each id — what sheep_build_tree_deg_dev needs to derive pst_weight
+ * from degrees instead of one atomic per record. */
+int sheep_degree_ex_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                        uint32_t* d_deg, uint32_t* d_selfc, void* stream);
+
 /* seq/rank from a degree vector (after an all-reduce for sharded input: sequence.h:78-91).
  * d_seq and d_rank hold n_ids entries.  Synchronises the stream; *n_seq_out is set. */
 int sheep_sequence_dev(const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq, uint32_t* d_rank,
@@ -95,6 +101,15 @@ int sheep_sequence_dev(const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq, u
  * the stream (the tree builder sizes its passes on the host). */
 int sheep_build_tree_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_ids,
                          uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst, void* stream);
+
+/* sheep_build_tree_dev with the degrees of THESE m records (d_deg, d_selfc from
+ * sheep_degree_ex_dev, in degree_mode) and d_seq (n_seq entries): pst_weight is derived as
+ * (non-self-loop degree) - (PREORDER records), with no per-record atomics.  For an edge shard,
+ * pass the shard's own (pre-all-reduce) degrees.  Synchronises the stream. */
+int sheep_build_tree_deg_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
+                             uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
+                             const uint32_t* d_deg, const uint32_t* d_selfc, int degree_mode,
+                             uint32_t* d_parent, uint32_t* d_pst, void* stream);
 
 /* In-place merge: (parent_a, pst_a) <- etree(A ∪ B).  Enqueue only. */
 int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_t* d_parent_b,

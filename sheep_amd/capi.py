@@ -60,7 +60,10 @@ def lib():
         "sheep_build_tree": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, u32p],
         "sheep_merge_trees": [u32p, u32p, u32p, u32p, c.c_uint32, u32p, u32p],
         "sheep_degree_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, vp],
+        "sheep_degree_ex_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, vp],
         "sheep_sequence_dev": [u32p, c.c_uint32, u32p, u32p, u32p, vp],
+        "sheep_build_tree_deg_dev": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, c.c_uint32, u32p,
+                                     u32p, c.c_int, u32p, u32p, vp],
         "sheep_build_tree_dev": [u32p, c.c_uint64, u32p, c.c_uint32, c.c_uint32, u32p, u32p, vp],
         "sheep_merge_trees_dev": [u32p, u32p, u32p, u32p, c.c_uint32, vp],
         "sheep_graph2tree_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, u32p, u32p,

@@ -142,16 +142,24 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 
 // Degree: LDS-bucketed histogram for large inputs, global atomics for small ones.
 static void degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
-                       uint32_t* d_deg, hipStream_t s) {
+                       uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s) {
   const char* e = getenv("SHEEP_DEGREE");
   bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
   if (!bucketed || n_ids == 0) {
-    launch_degree(d_uv, m, n_ids, mode, d_deg, c.d_err, s);
+    launch_degree(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, s);
     return;
   }
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
-  launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, nullptr, c.d_err, tmp, s);
+  launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s);
 }
+
+// Optional degree information for pst without per-edge atomics (launch_pst_from_degree).
+struct DegInfo {
+  const uint32_t* seq = nullptr;    // jnid -> vid
+  const uint32_t* deg = nullptr;    // degrees of THESE records
+  const uint32_t* selfc = nullptr;  // self-loop records per vid
+  int mode = SHEEP_DEGREE_LLAMA;
+};
 
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
                              uint32_t* d_rank, hipStream_t s) {
@@ -176,7 +184,7 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
 
 static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                            uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
-                           hipStream_t s, Timer* tm) {
+                           hipStream_t s, Timer* tm, const DegInfo* di = nullptr) {
   if (n_seq == 0) return;
   launch_fill(d_parent, INV, n_seq, s);
   launch_fill(d_pst, 0, n_seq, s);
@@ -186,7 +194,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
-  launch_edge_pass(d_uv, m, d_rank, n_rank, d_pst, items, c.d_err, s);
+  launch_edge_pass(d_uv, m, d_rank, n_rank, di ? nullptr : d_pst, items, c.d_err, s);
   if (tm) tm->mark("edge_pass");
   const char* ea = getenv("SHEEP_TREE_ALGO");
   bool kb = !(ea && strcmp(ea, "zip") == 0);
@@ -199,6 +207,12 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top, tmp, s);
   uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
   if (tm) tm->mark("bucket_sort");
+  if (di) {
+    uint32_t* rs = (uint32_t*)c.scratch.get("pst_start", (size_t)n_seq * 4);
+    uint32_t* re = (uint32_t*)c.scratch.get("pst_end", (size_t)n_seq * 4);
+    launch_pst_from_degree(sorted, m, di->seq, n_seq, di->deg, di->selfc, di->mode, rs, re, d_pst, s);
+    if (tm) tm->mark("pst");
+  }
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   if (!kb) {
     const char* ev = getenv("SHEEP_TREE_VARIANT");
@@ -339,7 +353,38 @@ int sheep_degree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degre
   require_aligned(d_uv, "d_uv");
   if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
     throw ApiError(-EINVAL, "degree_mode");
-  degree_dev(c, d_uv, m, n_ids, degree_mode, d_deg, pick(c, stream));
+  degree_dev(c, d_uv, m, n_ids, degree_mode, d_deg, nullptr, pick(c, stream));
+  API_END
+}
+
+int sheep_degree_ex_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                        uint32_t* d_deg, uint32_t* d_selfc, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  degree_dev(c, d_uv, m, n_ids, degree_mode, d_deg, d_selfc, pick(c, stream));
+  API_END
+}
+
+int sheep_build_tree_deg_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
+                             uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
+                             const uint32_t* d_deg, const uint32_t* d_selfc, int degree_mode,
+                             uint32_t* d_parent, uint32_t* d_pst, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  hipStream_t s = pick(c, stream);
+  Timer tm(s);
+  DegInfo di;
+  di.seq = d_seq;
+  di.deg = d_deg;
+  di.selfc = d_selfc;
+  di.mode = degree_mode;
+  build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, &tm, &di);
+  check_err(c, s);
+  tm.finish(c);
   API_END
 }
 
@@ -386,12 +431,18 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   hipStream_t s = pick(c, stream);
   Timer tm(s);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
+  uint32_t* selfc = (uint32_t*)c.scratch.get("selfc", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
-  degree_dev(c, d_uv, m, n_ids, degree_mode, deg, s);
+  degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s);
   tm.mark("degree");
   uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
   tm.mark("sequence");
-  build_tree_dev(c, d_uv, m, rank, n_ids, n_seq, d_parent, d_pst, s, &tm);
+  DegInfo di;
+  di.seq = d_seq;
+  di.deg = deg;
+  di.selfc = selfc;
+  di.mode = degree_mode;
+  build_tree_dev(c, d_uv, m, rank, n_ids, n_seq, d_parent, d_pst, s, &tm, &di);
   check_err(c, s);
   tm.finish(c);
   if (n_seq_out) *n_seq_out = n_seq;
@@ -424,7 +475,7 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
   uint32_t* seq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_ids * 4);
-  degree_dev(c, uv, m, n_ids, degree_mode, deg, s);
+  degree_dev(c, uv, m, n_ids, degree_mode, deg, nullptr, s);
   check_err(c, s);
   uint32_t n_seq = sequence_dev(c, deg, n_ids, seq, rank, s);
   if (n_seq) HIP_CHECK(hipMemcpyAsync(seq_out, seq, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));

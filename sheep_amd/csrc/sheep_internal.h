@@ -37,7 +37,11 @@ Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)
 
 // ---- launchers (sheep_kernels.hip); all enqueue on `s` -------------------------------------
 void launch_degree(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
-                   uint32_t* err, hipStream_t s);
+                   uint32_t* selfc, uint32_t* err, hipStream_t s);
+// pst = nsdeg - run length of r in the hi-sorted items (start/end: n_seq scratch words each)
+void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* seq, uint32_t n_seq,
+                            const uint32_t* deg, const uint32_t* selfc, int file_mode,
+                            uint32_t* start, uint32_t* end, uint32_t* pst, hipStream_t s);
 // Bucketed LDS degree histogram for large m (same result as launch_degree); selfc nullable.
 size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out);
 void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
@@ -59,7 +63,8 @@ void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s);
 void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
                          hipStream_t s);
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                      uint32_t* pst, uint64_t* items, uint32_t* err, hipStream_t s);
+                      uint32_t* pst /* nullable: no pst */, uint64_t* items, uint32_t* err,
+                      hipStream_t s);
 // variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
 void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
                         int variant, bool stats, unsigned long long* ws, hipStream_t s);

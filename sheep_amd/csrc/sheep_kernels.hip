@@ -39,22 +39,64 @@ static inline unsigned grid_for(uint64_t n, int per_block = BLOCK) {
 // always (sequence.h:105-106).
 // ---------------------------------------------------------------------------------------
 __global__ void k_degree(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode,
-                         uint32_t* __restrict__ deg, uint32_t* err) {
+                         uint32_t* __restrict__ deg, uint32_t* __restrict__ selfc, uint32_t* err) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint2 e = uv[i];
     if (e.x >= n_ids || e.y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
     atomicAdd(&deg[e.x], 1u);
     if (file_mode || e.x != e.y) atomicAdd(&deg[e.y], 1u);
+    if (selfc && e.x == e.y) atomicAdd(&selfc[e.x], 1u);
   }
 }
 
 void launch_degree(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
-                   uint32_t* err, hipStream_t s) {
+                   uint32_t* selfc, uint32_t* err, hipStream_t s) {
   if (n_ids) (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
+  if (n_ids && selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (m == 0) return;
   hipLaunchKernelGGL(k_degree, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, n_ids,
-                     file_mode, deg, err);
+                     file_mode, deg, selfc, err);
+}
+
+// pst_weight without per-edge atomics.  For the jnid r of vertex v = seq[r], the records at v
+// that are not self-loops are either PREORDER (other endpoint earlier in seq: r is their hi)
+// or POSTORDER (other endpoint later, or not in seq): jtree.cpp:78-87.  So
+//     pst[r] = nsdeg[v] - |{records with hi == r}|,   nsdeg[v] = deg[v] - w * selfloops[v]
+// (w = 1 for LLAMA degrees, 2 for FILE degrees), and the second term is the length of r's run
+// in the hi-sorted edge list.
+__global__ void k_run_bounds(const uint64_t* __restrict__ items, uint64_t m,
+                             uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    uint32_t b = (uint32_t)(items[i] >> 32);
+    if (b == INV) continue;
+    uint32_t pb = i ? (uint32_t)(items[i - 1] >> 32) : INV;
+    uint32_t nb = i + 1 < m ? (uint32_t)(items[i + 1] >> 32) : INV;
+    if (b != pb) start[b] = (uint32_t)i;
+    if (b != nb) end[b] = (uint32_t)(i + 1);
+  }
+}
+
+__global__ void k_pst_from_degree(const uint32_t* __restrict__ seq, uint32_t n_seq,
+                                  const uint32_t* __restrict__ deg, const uint32_t* __restrict__ selfc,
+                                  uint32_t w, const uint32_t* __restrict__ start,
+                                  const uint32_t* __restrict__ end, uint32_t* __restrict__ pst) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_seq; r += gridDim.x * blockDim.x) {
+    uint32_t v = seq[r];
+    pst[r] = deg[v] - w * selfc[v] - (end[r] - start[r]);
+  }
+}
+
+void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* seq, uint32_t n_seq,
+                            const uint32_t* deg, const uint32_t* selfc, int file_mode,
+                            uint32_t* start, uint32_t* end, uint32_t* pst, hipStream_t s) {
+  if (n_seq == 0) return;
+  (void)hipMemsetAsync(start, 0, (size_t)n_seq * 4, s);
+  (void)hipMemsetAsync(end, 0, (size_t)n_seq * 4, s);
+  if (m) hipLaunchKernelGGL(k_run_bounds, dim3(grid_for(m)), dim3(BLOCK), 0, s, sorted, m, start, end);
+  hipLaunchKernelGGL(k_pst_from_degree, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, seq, n_seq, deg,
+                     selfc, file_mode ? 2u : 1u, (const uint32_t*)start, (const uint32_t*)end, pst);
 }
 
 // stats[0] = max degree, stats[1] = number of zero-degree ids.
@@ -540,22 +582,21 @@ void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, ui
 // ---------------------------------------------------------------------------------------
 __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
                             const uint32_t* __restrict__ rank, uint32_t n_rank,
-                            uint32_t* __restrict__ pst, uint64_t* __restrict__ items, uint32_t* err,
-                            int ablate) {
+                            uint32_t* __restrict__ pst, uint64_t* __restrict__ items, uint32_t* err) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     uint2 e = uv[i];
     uint32_t hi = INV, lo = INV;
     if (e.x != e.y) {
       bool ox = e.x >= n_rank, oy = e.y >= n_rank;
-      uint32_t rx = ox ? INV : ((ablate & 2) ? e.x : rank[e.x]);
-      uint32_t ry = oy ? INV : ((ablate & 2) ? e.y : rank[e.y]);
+      uint32_t rx = ox ? INV : rank[e.x];
+      uint32_t ry = oy ? INV : rank[e.y];
       if ((ox && ry != INV) || (oy && rx != INV)) {
         atomicOr(err, ERR_RANGE);
       } else {
         lo = min(rx, ry);
         hi = max(rx, ry);
-        if (lo != INV && !(ablate & 1)) atomicAdd(&pst[lo], 1u);
+        if (lo != INV && pst) atomicAdd(&pst[lo], 1u);
       }
     }
     items[i] = ((uint64_t)hi << 32) | lo;
@@ -565,9 +606,8 @@ __global__ void k_edge_pass(const uint2* __restrict__ uv, uint64_t m,
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                       uint32_t* pst, uint64_t* items, uint32_t* err, hipStream_t s) {
   if (m == 0) return;
-  const char* ea = getenv("SHEEP_EP_ABLATE");  // diagnostics only: 1 = no pst, 2 = no gathers
   hipLaunchKernelGGL(k_edge_pass, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, rank,
-                     n_rank, pst, items, err, ea ? atoi(ea) : 0);
+                     n_rank, pst, items, err);
 }
 
 // ---------------------------------------------------------------------------------------

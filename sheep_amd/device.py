@@ -38,6 +38,24 @@ def degree(uv, n_ids, mode=capi.DEGREE_LLAMA, out=None):
     return deg
 
 
+def degree_ex(uv, n_ids, mode=capi.DEGREE_LLAMA):
+    """(deg, selfc): degrees and self-loop record counts of these records."""
+    deg = torch.empty(max(n_ids, 1), dtype=torch.uint32, device=uv.device)
+    selfc = torch.empty(max(n_ids, 1), dtype=torch.uint32, device=uv.device)
+    capi.call("sheep_degree_ex_dev", _p(uv), uv.shape[0], n_ids, mode, _p(deg), _p(selfc),
+              _stream())
+    return deg[:n_ids], selfc[:n_ids]
+
+
+def build_tree_deg(uv, rank, seq, n_seq, deg, selfc, mode=capi.DEGREE_LLAMA):
+    """build_tree with pst derived from these records' own degrees (no per-edge atomics)."""
+    parent = torch.empty(max(n_seq, 1), dtype=torch.uint32, device=uv.device)
+    pst = torch.empty(max(n_seq, 1), dtype=torch.uint32, device=uv.device)
+    capi.call("sheep_build_tree_deg_dev", _p(uv), uv.shape[0], _p(rank), rank.numel(), _p(seq),
+              n_seq, _p(deg), _p(selfc), mode, _p(parent), _p(pst), _stream())
+    return parent, pst
+
+
 def sequence(deg, seq=None, rank=None):
     n_ids = deg.numel()
     seq = seq if seq is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=deg.device)

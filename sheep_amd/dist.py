@@ -30,11 +30,13 @@ def build_tree_sharded(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     """Returns (seq, parent, pst, n_seq) on rank 0 and (seq, None, None, n_seq) elsewhere."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    deg = ops.degree(uv_shard, n_ids, mode)
+    deg_local, selfc = ops.degree(uv_shard, n_ids, mode)
+    deg = deg_local.clone() if world > 1 else deg_local
     if world > 1:
         dist.all_reduce(_i32(deg), op=dist.ReduceOp.SUM, group=group)
     seq, rmap, n_seq = ops.sequence(deg)
-    parent, pst = ops.build_tree(uv_shard, rmap, n_seq)
+    # pst of the partial tree comes from this shard's own degrees (pre-all-reduce)
+    parent, pst = ops.build_tree(uv_shard, rmap, seq, n_seq, deg_local, selfc, mode)
     step = 1
     while step < world:
         if rank % (2 * step) == 0:
@@ -62,13 +64,13 @@ class DeviceOps:
         self.d = device
 
     def degree(self, uv, n_ids, mode):
-        return self.d.degree(uv, n_ids, mode)
+        return self.d.degree_ex(uv, n_ids, mode)
 
     def sequence(self, deg):
         return self.d.sequence(deg)
 
-    def build_tree(self, uv, rmap, n_seq):
-        return self.d.build_tree(uv, rmap, n_seq)
+    def build_tree(self, uv, rmap, seq, n_seq, deg_local, selfc, mode):
+        return self.d.build_tree_deg(uv, rmap, seq, n_seq, deg_local, selfc, mode)
 
     def merge_into(self, pa, sa, pb, sb, n):
         self.d.merge_into(pa, sa, pb, sb, n)

@@ -20,7 +20,8 @@ class CheckerOps:
         self.seq = None
 
     def degree(self, uv, n_ids, mode):
-        return torch.from_numpy(self.O.degree(uv.numpy(), mode, n_ids).astype(np.uint32))
+        deg = torch.from_numpy(self.O.degree(uv.numpy(), mode, n_ids).astype(np.uint32))
+        return deg, torch.zeros_like(deg)
 
     def sequence(self, deg):
         self.seq = self.O.sequence(deg.numpy().astype(np.uint32))
@@ -28,7 +29,7 @@ class CheckerOps:
         rmap[self.seq] = np.arange(len(self.seq), dtype=np.uint32)
         return torch.from_numpy(self.seq.copy()), torch.from_numpy(rmap), len(self.seq)
 
-    def build_tree(self, uv, rmap, n_seq):
+    def build_tree(self, uv, rmap, seq, n_seq, deg_local, selfc, mode):
         p, s = self.O.build_tree(uv.numpy(), self.seq)
         return torch.from_numpy(p.copy()), torch.from_numpy(s.copy())
 

@@ -181,3 +181,44 @@ def test_degree_paths_agree(oracle, api, monkeypatch, path, seed):
     uv[hub, 0] = 1
     for mode in (0, 1):
         assert np.array_equal(api.degree_sequence(uv, mode), oracle.degree_sequence(uv, mode))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sharded_partial_trees_with_degree_pst(oracle, gpu, seed):
+    """sheep_degree_ex_dev + sheep_build_tree_deg_dev on edge shards (the multi-GPU per-rank
+    step) equal the checker's partial trees, and their merges equal the whole tree."""
+    import torch
+    from sheep_amd import device
+
+    scale, P = 13, 3
+    uv_all = device.rmat(scale, 16, 40 + seed)
+    uv = uv_all.cpu().numpy().view(np.uint32)
+    # add self-loops and an id-space gap so the self-loop and missing-id paths are exercised
+    uv = np.concatenate([uv, np.array([[5, 5], [5, 5], [7, 7]], np.uint32)])
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    n_ids = 1 << scale
+    deg = torch.zeros(n_ids, dtype=torch.uint32, device="cuda")
+    shards = []
+    R = len(uv)
+    for r in range(P):
+        sh = uv_d[R * r // P: R * (r + 1) // P].contiguous()
+        d, sc = device.degree_ex(sh, n_ids)
+        deg = (deg.view(torch.int32) + d.view(torch.int32)).view(torch.uint32)
+        shards.append((sh, d, sc))
+    seq, rank, n_seq = device.sequence(deg)
+    oseq = oracle.degree_sequence(uv)
+    assert n_seq == len(oseq) and np.array_equal(seq[:n_seq].cpu().numpy().view(np.uint32), oseq)
+    acc = None
+    for r, (sh, d, sc) in enumerate(shards):
+        p, s = device.build_tree_deg(sh, rank, seq, n_seq, d, sc)
+        op, os_ = oracle.build_tree(uv[R * r // P: R * (r + 1) // P], oseq)
+        assert np.array_equal(p[:n_seq].cpu().numpy().view(np.uint32), op)
+        assert np.array_equal(s[:n_seq].cpu().numpy().view(np.uint32), os_)
+        if acc is None:
+            acc = (p, s)
+        else:
+            device.merge_into(acc[0], acc[1], p, s, n_seq)
+    torch.cuda.synchronize()
+    wp, ws = oracle.build_tree(uv, oseq)
+    assert np.array_equal(acc[0][:n_seq].cpu().numpy().view(np.uint32), wp)
+    assert np.array_equal(acc[1][:n_seq].cpu().numpy().view(np.uint32), ws)
