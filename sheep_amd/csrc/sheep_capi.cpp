@@ -203,7 +203,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   int top = bits_for(n_seq);
   // kb needs edges fully sorted by hi (bucket ranges + wave dedupe); the plain zipper only
   // needs them bucketed by the top 16 bits (order affects work, never the result).
-  int lo_bit = kb ? 0 : std::max(0, top - 16);
+  // (pst from degrees also needs the full sort: it counts each hi's run.)
+  int lo_bit = (kb || di) ? 0 : std::max(0, top - 16);
   const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top, tmp, s);
   uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
   if (tm) tm->mark("bucket_sort");
