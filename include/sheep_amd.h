@@ -11,8 +11,8 @@
  *   - the caller owns every buffer; the library owns its device scratch (grown on demand,
  *     released by sheep_release());
  *   - host-pointer calls are synchronous; *_dev calls take device pointers and a HIP stream
- *     (hipStream_t passed as void*, NULL = the library's stream) and return when the work is
- *     ENQUEUED, except where a host-side count is returned (documented per call);
+ *     (hipStream_t passed as void*; NULL = HIP's default stream, as everywhere in HIP) and
+ *     return when the work is ENQUEUED, except where documented as synchronising;
  *   - calls are not re-entrant per device.
  *
  * Types follow lib/defs.h:76-82: ids, jnids and weights are uint32, INVALID = 0xFFFFFFFF.

@@ -91,8 +91,11 @@ Ctx& ctx() {
   return g_ctx[g_device];
 }
 
+// Device-pointer calls run on the caller's stream; NULL is HIP's default (null) stream, as
+// for any HIP API (torch's default stream handle is 0).  Host-pointer calls use c.stream.
 static hipStream_t pick(Ctx& c, void* stream) {
-  return stream ? (hipStream_t)stream : c.stream;
+  (void)c;
+  return (hipStream_t)stream;
 }
 
 // Phase timing with HIP events on the working stream.
