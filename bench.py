@@ -39,6 +39,17 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def pmc_traffic(kernel, scale):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/), if one was
+    collected for this workload: FETCH_SIZE and WRITE_SIZE from separate rocprofv3 --pmc passes."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(path))["rmat%d" % scale][kernel]
+        return rec["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(scale, edgefactor, seed):
     """Single-thread CPU restatement of graph2tree's Sorted+Mapped window (oracle, the
     reference's algorithm with FastUnionFind) on a bounded sample: R-MAT `scale`."""
@@ -119,22 +130,18 @@ def main():
         ms_per_step = 1e3 * elapsed / args.steps
         n_seq = out[3] if world > 1 else out[3]
         value = m / (elapsed / args.steps)
-        # Roofline of the dominant kernel (timed with HIP events on the library's stream, inside
-        # the timed steps).  Algorithmic bytes per launch are defined in DESIGN.md §Roofline.
+        # Roofline of the dominant single kernel, k_edge_pass (one launch per step; its phase
+        # is bracketed by HIP events on the stream it runs on).  Algorithmic bytes per launch
+        # (DESIGN.md §5): 8 B record read + 8 B item written + 2 x 4 B rank words gathered.
         avg = {k: sum(v) / len(v) for k, v in phase.items()}
-        algo = {
-            "tree_insert": 8 * m + 4 * n_seq,          # sorted (hi,lo) in, parent out
-            "bucket_sort": 2 * 2 * 8 * m,              # 2 radix passes x (read+write 8 B/rec)
-            "edge_pass": 8 * m + 8 * m + 4 * n_seq,    # records in, (hi,lo) out, pst
-            "sequence": 2 * 16 * n_ids,                # <=2 radix passes over (deg,id)
-            "degree": 8 * m + 4 * n_ids,               # records in, degree out
-        }
-        dom = max(avg, key=avg.get) if avg else None
         roof = None
-        if dom:
-            ach = algo.get(dom, 0) / (avg[dom] * 1e-3)
-            roof = {"kernel": dom, "bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9,
-                    "unit": "GB/s", "frac": ach / HBM_PEAK, "traffic": None,
+        if "edge_pass" in avg:
+            algo = 24 * (hi - lo) if world > 1 else 24 * m
+            ach = algo / (avg["edge_pass"] * 1e-3)
+            roof = {"kernel": "k_edge_pass", "bound": "hbm", "achieved": ach / 1e9,
+                    "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
+                    "traffic": pmc_traffic("k_edge_pass", scale), "algo_bytes": algo,
+                    "avg_ms": avg["edge_pass"],
                     "phases_ms": {k: round(v, 3) for k, v in avg.items()}}
         path_bytes = 16 * m + 24 * n_seq  # SURVEY §8d B(m, n)
         rec = {

@@ -197,6 +197,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
+  if (tm) tm->mark("tree_init");
   launch_edge_pass(d_uv, m, d_rank, n_rank, di ? nullptr : d_pst, items, c.d_err, s);
   if (tm) tm->mark("edge_pass");
   const char* ea = getenv("SHEEP_TREE_ALGO");
