@@ -410,54 +410,62 @@ static constexpr int RS_ITEMS = 8;
 static constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 static constexpr int RS_WAVES = RS_THREADS / 64;
 
+template <int DB>  // digit bits: 8 or 9
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* __restrict__ counts,
               uint32_t ntiles) {
-  __shared__ uint32_t hist[256];
-  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+  constexpr uint32_t NBIN = 1u << DB;
+  __shared__ uint32_t hist[NBIN];
+  for (uint32_t i = threadIdx.x; i < NBIN; i += RS_THREADS) hist[i] = 0;
   __syncthreads();
   uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
     uint64_t idx = base + (uint64_t)i * RS_THREADS + threadIdx.x;
-    if (idx < n) atomicAdd(&hist[(uint32_t)(in[idx] >> (32 + shift)) & 255u], 1u);
+    if (idx < n) atomicAdd(&hist[(uint32_t)(in[idx] >> (32 + shift)) & (NBIN - 1)], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < 256) counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < NBIN; i += RS_THREADS)
+    counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
+template <int DB>
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n, int shift,
                 const uint32_t* __restrict__ offsets, uint32_t ntiles) {
+  constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint64_t stage[RS_TILE];
-  __shared__ uint32_t whist[RS_WAVES][256];
-  __shared__ uint32_t tstart[256], running[256], goff[256], wsum[RS_WAVES];
+  __shared__ uint32_t whist[RS_WAVES][NBIN];
+  __shared__ uint32_t tstart[NBIN], running[NBIN], goff[NBIN], wsum[RS_WAVES];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
   const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
   uint64_t item[RS_ITEMS];
   uint32_t dg[RS_ITEMS];
-  if (t < 256) { running[t] = 0; goff[t] = offsets[(uint64_t)t * ntiles + blockIdx.x]; }
-  for (int i = t; i < RS_WAVES * 256; i += RS_THREADS) (&whist[0][0])[i] = 0;
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS) {
+    running[i] = 0;
+    goff[i] = offsets[(uint64_t)i * ntiles + blockIdx.x];
+  }
+  for (int i = t; i < RS_WAVES * (int)NBIN; i += RS_THREADS) (&whist[0][0])[i] = 0;
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
     uint32_t li = (uint32_t)i * RS_THREADS + t;
     item[i] = li < tile_n ? in[base + li] : 0ull;
-    dg[i] = (uint32_t)(item[i] >> (32 + shift)) & 255u;
+    dg[i] = (uint32_t)(item[i] >> (32 + shift)) & (NBIN - 1);
   }
   __syncthreads();
-  // tile digit totals -> tstart (exclusive); reuse whist[0] as the histogram
+  // tile digit totals -> tstart (exclusive); whist[0] doubles as the histogram
   for (int i = 0; i < RS_ITEMS; ++i)
     if ((uint32_t)i * RS_THREADS + t < tile_n) atomicAdd(&whist[0][dg[i]], 1u);
   __syncthreads();
-  if (t < 256) {
+  if (t < (int)NBIN) {
     uint32_t v = whist[0][t];
     uint32_t incl = wave_incl_scan(v);
     if (lane == 63) wsum[w] = incl;
-    tstart[t] = incl - v;  // within-wave exclusive; waves 0..3 cover the 256 digits
+    tstart[t] = incl - v;
   }
   __syncthreads();
-  if (t < 256) {
+  if (t < (int)NBIN) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
@@ -471,7 +479,7 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
     uint32_t d = dg[c];
     uint64_t match = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < DB; ++b) {
       bool bit = (d >> b) & 1u;
       uint64_t bal = __ballot(bit);
       match &= bit ? bal : ~bal;
@@ -485,42 +493,55 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
       stage[pos] = item[c];
     }
     __syncthreads();
-    if (t < 256) {
+    for (uint32_t dd = t; dd < NBIN; dd += RS_THREADS) {
       uint32_t tot = 0;
-      for (int i = 0; i < RS_WAVES; ++i) { tot += whist[i][t]; whist[i][t] = 0; }
-      running[t] += tot;
+      for (int i = 0; i < RS_WAVES; ++i) { tot += whist[i][dd]; whist[i][dd] = 0; }
+      running[dd] += tot;
     }
     __syncthreads();
   }
   for (uint32_t j = t; j < tile_n; j += RS_THREADS) {
     uint64_t it = stage[j];
-    uint32_t d = (uint32_t)(it >> (32 + shift)) & 255u;
+    uint32_t d = (uint32_t)(it >> (32 + shift)) & (NBIN - 1);
     out[(uint64_t)goff[d] + (j - tstart[d])] = it;
   }
 }
 
 size_t rsort_tmp_words(uint64_t n) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
-  return 256 * nt + scan_tmp_words(256 * nt);
+  return 512 * nt + scan_tmp_words(512 * nt);
 }
 
-// Sorts n items on bits [bit_lo, bit_hi) of their upper word; returns the buffer holding the
-// result (in, a or b).  `in` is never written.
+// Sorts n items on bits [bit_lo, bit_hi) of their upper word with passes of <= 9 bits (25 bits
+// -> 9+8+8); returns the buffer holding the result (in, a or b).  `in` is never written.
 uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
                          int bit_hi, uint32_t* tmp, hipStream_t s) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
-  uint32_t* stmp = tmp + 256 * nt;
+  uint32_t* stmp = tmp + 512 * nt;
   const uint64_t* src = in;
   uint64_t* dst = a;
-  for (int shift = bit_lo; shift < bit_hi; shift += 8) {
+  int bits = bit_hi - bit_lo;
+  int passes = bits > 0 ? (bits + 8) / 9 : 0;
+  for (int p = 0, shift = bit_lo; p < passes; ++p) {
+    int width = (bits - (shift - bit_lo)) / (passes - p);          // even split, wider first
+    if ((bits - (shift - bit_lo)) % (passes - p)) width += 1;
     if (n) {
-      hipLaunchKernelGGL(k_rsort_count, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n, shift,
-                         counts, (uint32_t)nt);
-      launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
-      hipLaunchKernelGGL(k_rsort_scatter, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst, n,
-                         shift, (const uint32_t*)counts, (uint32_t)nt);
+      if (width > 8) {
+        hipLaunchKernelGGL(k_rsort_count<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+                           shift, counts, (uint32_t)nt);
+        launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
+        hipLaunchKernelGGL(k_rsort_scatter<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt);
+      } else {
+        hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+                           shift, counts, (uint32_t)nt);
+        launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
+        hipLaunchKernelGGL(k_rsort_scatter<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt);
+      }
     }
+    shift += width;
     src = dst;
     dst = (dst == a) ? b : a;
   }
