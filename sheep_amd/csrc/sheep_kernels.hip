@@ -765,15 +765,29 @@ __global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint
 // one global counter (one atomic per 512 edges) and every lane that finishes an edge takes
 // the next one at the following step, so a wave never idles behind its slowest lane.
 // Edge source of the queue: packed u64 items (hi << 32 | lo) or two u32 arrays.
+__device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
+                                                 uint32_t G);
+
 struct EdgeSrc {
   const uint64_t* items;  // packed (hi << 32 | lo)
   const uint32_t* hi;     // or hi[] / lo[]
   const uint32_t* lo;
-  uint32_t base = 0;      // or (items == hi == nullptr): b = base + i, a = lo[i]
+  // kb bucket mode (items == nullptr): indices [0, np) are the giant's path slots (rank
+  // B0 + i, edge (pred, B0 + i) when marked in `bitmap`), then [np, np + nk) the kept pairs.
+  const uint32_t* bitmap = nullptr;
+  uint32_t B0 = 0, G = INV;
+  uint64_t np = 0;
   __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a) const {
-    if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; }
-    else if (hi) { b = hi[i]; a = (b != INV) ? lo[i] : 0u; }
-    else { a = lo[i]; b = (a != INV) ? base + (uint32_t)i : INV; }
+    if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; return; }
+    if (i < np) {
+      b = B0 + (uint32_t)i;
+      if ((bitmap[b >> 5] >> (b & 31)) & 1u) a = kb_path_pred(bitmap, B0, b, G);
+      else b = INV, a = 0;
+      return;
+    }
+    i -= np;
+    b = hi[i];
+    a = (b != INV) ? lo[i] : 0u;
   }
 };
 
@@ -840,20 +854,6 @@ __global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uin
   tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, next, stats, ZRec());
 }
 
-// The kb in-bucket pass: the kept (g, b) list of a bucket (count on the device) through the
-// balanced lane queue, recording pre-bucket roots it links.
-template <bool STATS>
-__global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
-                         uint32_t kbase, uint64_t n, uint32_t* parent, uint32_t* jump,
-                         unsigned long long* next, unsigned long long* stats, uint32_t B0,
-                         uint32_t* linked, uint32_t* n_linked) {
-  ZRec rec;
-  rec.B0 = B0;
-  rec.linked = linked;
-  rec.n_linked = n_linked;
-  EdgeSrc src{nullptr, kb, kg, kbase};
-  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
-}
 
 typedef void (*TreeKernel)(const uint64_t*, uint64_t, uint32_t*, uint32_t*, unsigned long long*,
                            unsigned long long*);
@@ -988,7 +988,7 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
                          uint32_t* bitmap, unsigned long long* stats, int mapmode) {
   // G: the component of the last pre-bucket vertex (in a degree-ordered sequence: the giant).
   // Its (G, b) pairs go to a rank bitmap and become path edges (k_kb_path), not zipper walks.
-  const uint32_t G = (B0 > 0 && mapmode == 4) ? label[uf_find<false>(uf, B0 - 1)] : INV;
+  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find<false>(uf, B0 - 1)] : INV;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -1032,46 +1032,55 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
   }
 }
 
-// Star -> path for the giant: G is adjacent to the marked ranks b1 < b2 < ... of the bucket.
-// For the etree that star is equivalent to the path G-b1-b2-...: at any threshold both
-// connect G with exactly the marked ranks present.  So each marked b gets the edge
-// (previous marked rank, b); if none is found within 64 words back, (G, b) — always valid,
-// only a longer walk.  pa[b] = the lower endpoint (INVALID for unmarked ranks).
-__device__ __forceinline__ void kb_path_body(uint32_t* __restrict__ bitmap, uint32_t B0,
-                                             uint32_t B1, uint32_t G, uint32_t* __restrict__ pa) {
-  const uint32_t w0 = B0 >> 5, w1 = (B1 + 31) >> 5;
-  for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += gridDim.x * blockDim.x) {
-    uint32_t bits = bitmap[w];
-    uint32_t lo_mask = (w == w0) ? (~0u << (B0 & 31)) : ~0u;
-    uint32_t hi_mask = (w == w1 - 1 && (B1 & 31)) ? ((1u << (B1 & 31)) - 1u) : ~0u;
-    bits &= lo_mask & hi_mask;
-    if (!bits) continue;
-    uint32_t pred = G;  // predecessor of this word's first marked rank
-    for (uint32_t v = w, k = 0; v > w0 && k < 64; --v, ++k) {
-      uint32_t pb = bitmap[v - 1] & ((v - 1 == w0) ? (~0u << (B0 & 31)) : ~0u);
-      if (pb) { pred = ((v - 1) << 5) + 31 - __clz(pb); break; }
-    }
-    for (uint32_t rem = bits; rem;) {
-      uint32_t b = (w << 5) + (__ffs(rem) - 1);
-      rem &= rem - 1;
-      pa[b] = pred;
-      pred = b;
-    }
+// Star -> path for the giant G: G is adjacent to the marked ranks b1 < b2 < ... of the bucket.
+// For the etree that star is equivalent to the path G-b1-b2-...: at every threshold both
+// connect G with exactly the marked ranks present.  So a marked b gets the edge
+// (previous marked rank, b) — a walk that starts next to its target — or (G, b) for the first
+// (also when none is found within 64 words back: always valid, only a longer walk).
+__device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
+                                                 uint32_t G) {
+  const uint32_t w0 = B0 >> 5, w = b >> 5;
+  uint32_t lo_mask = (w == w0) ? (~0u << (B0 & 31)) : ~0u;
+  uint32_t bits = bitmap[w] & lo_mask & ((1u << (b & 31)) - 1u);
+  if (bits) return (w << 5) + 31 - __clz(bits);
+  for (uint32_t v = w, k = 0; v > w0 && k < 64; --v, ++k) {
+    uint32_t pb = bitmap[v - 1] & ((v - 1 == w0) ? (~0u << (B0 & 31)) : ~0u);
+    if (pb) return ((v - 1) << 5) + 31 - __clz(pb);
   }
+  return G;
 }
 
-__global__ void k_kb_giant(uint32_t* uf, const uint32_t* __restrict__ label, uint32_t B0, uint32_t* G) {
-  if (threadIdx.x == 0) *G = label[uf_find<false>(uf, B0 - 1)];
-}
-
-__global__ void k_kb_path(uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
-                          const uint32_t* __restrict__ G, uint32_t* __restrict__ pa) {
-  kb_path_body(bitmap, B0, B1, *G, pa);
+// The kb in-bucket pass: the kept (g, b) list of a bucket (count on the device) through the
+// balanced lane queue, recording pre-bucket roots it links.
+template <bool STATS>
+__global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
+                         uint64_t nk, const uint32_t* __restrict__ bitmap, uint32_t B1,
+                         uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
+                         uint32_t* jump, unsigned long long* next, unsigned long long* stats,
+                         uint32_t B0, uint32_t* linked, uint32_t* n_linked, int giant) {
+  ZRec rec;
+  rec.B0 = B0;
+  rec.linked = linked;
+  rec.n_linked = n_linked;
+  EdgeSrc src{nullptr, kb, kg};
+  if (giant && B0 > 0) {
+    src.bitmap = bitmap;
+    src.B0 = B0;
+    src.G = label[uf_find<false>(uf, B0 - 1)];
+    src.np = B1 - B0;
+  }
+  uint64_t n = src.np + nk;
+  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
 }
 
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
                            uint32_t B1, const uint32_t* __restrict__ linked,
-                           const uint32_t* __restrict__ n_linked) {
+                           const uint32_t* __restrict__ n_linked, uint32_t* bitmap) {
+  // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
+  // with the next bucket hold no marks of it yet; the previous bucket cleared its own)
+  for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
+       w += gridDim.x * blockDim.x)
+    bitmap[w] = 0;
   const uint32_t nl = *n_linked, width = B1 - B0;
   const uint64_t total = (uint64_t)width + nl;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -1131,39 +1140,29 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* pa, uint32_t* counters, bool stats,
+                      uint32_t* bitmap, uint32_t* counters, bool stats,
                       unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
-  int mapmode = em ? atoi(em) : 0;
-  // counters: [1] n_linked, [3] G for the path kernel, [4..5] unused u64
+  int mapmode = em ? atoi(em) : 0;  // 0: giant star->path on; 3: off
+  // counters: [1] n_linked, [4..5] unused queue cursor
   uint32_t* n_linked = counters + 1;
   unsigned long long* next = (unsigned long long*)(counters + 4);
   (void)hipMemsetAsync(counters, 0, 16, s);
-  auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
   if (e_end > e_begin) {
     uint64_t waves = (e_end - e_begin + 63) / 64;
     unsigned grid = grid_for(waves * 64);
     auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
     hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
                        (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
-    if (B0 > 0 && mapmode == 4) {
-      hipLaunchKernelGGL(k_kb_giant, dim3(1), dim3(64), 0, s, uf, (const uint32_t*)label, B0,
-                         counters + 3);
-      hipLaunchKernelGGL(k_kb_path, dim3(grid_for(((B1 - B0) >> 5) + 2)), dim3(BLOCK), 0, s,
-                         bitmap, B0, B1, (const uint32_t*)(counters + 3), pa);
-      hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)nullptr,
-                         (const uint32_t*)(pa + B0), B0, (uint64_t)(B1 - B0), parent, jump, next,
-                         st + 8, B0, linked, n_linked);
-      (void)hipMemsetAsync(bitmap + (B0 >> 5), 0, (size_t)(((B1 + 31) >> 5) - (B0 >> 5)) * 4, s);
-      (void)hipMemsetAsync(pa + B0, 0xFF, (size_t)(B1 - B0) * 4, s);
-    }
+    auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
-                       (const uint32_t*)kept_g, 0u, e_end - e_begin, parent, jump, next, st + 8,
-                       B0, linked, n_linked);
+                       (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap, B1, uf,
+                       (const uint32_t*)label, parent, jump, next, st + 8, B0, linked, n_linked,
+                       mapmode == 0 ? 1 : 0);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
-                     (const uint32_t*)linked, (const uint32_t*)n_linked);
+                     (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, n_linked);
 }
