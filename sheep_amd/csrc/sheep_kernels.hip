@@ -766,7 +766,7 @@ __global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint
 // the next one at the following step, so a wave never idles behind its slowest lane.
 // Edge source of the queue: packed u64 items (hi << 32 | lo) or two u32 arrays.
 __device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
-                                                 uint32_t G);
+                                                 uint32_t G, uint32_t limit);
 
 struct EdgeSrc {
   const uint64_t* items;  // packed (hi << 32 | lo)
@@ -775,13 +775,13 @@ struct EdgeSrc {
   // kb bucket mode (items == nullptr): indices [0, np) are the giant's path slots (rank
   // B0 + i, edge (pred, B0 + i) when marked in `bitmap`), then [np, np + nk) the kept pairs.
   const uint32_t* bitmap = nullptr;
-  uint32_t B0 = 0, G = INV;
+  uint32_t B0 = 0, G = INV, limit = 64;
   uint64_t np = 0;
   __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a) const {
     if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; return; }
     if (i < np) {
       b = B0 + (uint32_t)i;
-      if ((bitmap[b >> 5] >> (b & 31)) & 1u) a = kb_path_pred(bitmap, B0, b, G);
+      if ((bitmap[b >> 5] >> (b & 31)) & 1u) a = kb_path_pred(bitmap, B0, b, G, limit);
       else b = INV, a = 0;
       return;
     }
@@ -1038,12 +1038,12 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
 // (previous marked rank, b) — a walk that starts next to its target — or (G, b) for the first
 // (also when none is found within 64 words back: always valid, only a longer walk).
 __device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
-                                                 uint32_t G) {
+                                                 uint32_t G, uint32_t limit) {
   const uint32_t w0 = B0 >> 5, w = b >> 5;
   uint32_t lo_mask = (w == w0) ? (~0u << (B0 & 31)) : ~0u;
   uint32_t bits = bitmap[w] & lo_mask & ((1u << (b & 31)) - 1u);
   if (bits) return (w << 5) + 31 - __clz(bits);
-  for (uint32_t v = w, k = 0; v > w0 && k < 64; --v, ++k) {
+  for (uint32_t v = w, k = 0; v > w0 && k < limit; --v, ++k) {
     uint32_t pb = bitmap[v - 1] & ((v - 1 == w0) ? (~0u << (B0 & 31)) : ~0u);
     if (pb) return ((v - 1) << 5) + 31 - __clz(pb);
   }
@@ -1057,7 +1057,8 @@ __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __rest
                          uint64_t nk, const uint32_t* __restrict__ bitmap, uint32_t B1,
                          uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
                          uint32_t* jump, unsigned long long* next, unsigned long long* stats,
-                         uint32_t B0, uint32_t* linked, uint32_t* n_linked, int giant) {
+                         uint32_t B0, uint32_t* linked, uint32_t* n_linked, int giant,
+                         uint32_t scan_limit) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
@@ -1068,6 +1069,7 @@ __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __rest
     src.B0 = B0;
     src.G = label[uf_find<false>(uf, B0 - 1)];
     src.np = B1 - B0;
+    src.limit = scan_limit;
   }
   uint64_t n = src.np + nk;
   tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
@@ -1144,6 +1146,8 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
   int mapmode = em ? atoi(em) : 0;  // 0: giant star->path on; 3: off
+  const char* esl = getenv("SHEEP_KB_SCAN");
+  uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
   // counters: [1] n_linked, [4..5] unused queue cursor
   uint32_t* n_linked = counters + 1;
   unsigned long long* next = (unsigned long long*)(counters + 4);
@@ -1158,7 +1162,7 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
                        (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap, B1, uf,
                        (const uint32_t*)label, parent, jump, next, st + 8, B0, linked, n_linked,
-                       mapmode == 0 ? 1 : 0);
+                       mapmode == 0 ? 1 : 0, scan_limit);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
