@@ -791,12 +791,14 @@ struct EdgeSrc {
   }
 };
 
+// Queue chunk (edges per wave refill): all waves sweep the list together, so about
+// nwaves * chunk edges are in flight — the concurrency window that the zipper's rework grows
+// with.  Set per launch by the host (qchunk).
 template <int LOAD, int JUMP, bool STATS, bool REC>
 __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
                                                 uint32_t* parent, uint32_t* jump,
                                                 unsigned long long* next, unsigned long long* stats,
-                                                const ZRec& rec) {
-  constexpr uint32_t CH = 64 * 8;
+                                                const ZRec& rec, uint32_t CH = 512) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t cbase = 0, cend = 0;  // wave-uniform chunk cursor
@@ -1058,7 +1060,7 @@ __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __rest
                          uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
                          uint32_t* jump, unsigned long long* next, unsigned long long* stats,
                          uint32_t B0, uint32_t* linked, uint32_t* n_linked, int giant,
-                         uint32_t scan_limit) {
+                         uint32_t scan_limit, uint32_t qchunk) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
@@ -1072,7 +1074,7 @@ __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __rest
     src.limit = scan_limit;
   }
   uint64_t n = src.np + nk;
-  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec);
+  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec, qchunk);
 }
 
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
@@ -1145,7 +1147,7 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t* bitmap, uint32_t* counters, bool stats,
                       unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
-  int mapmode = em ? atoi(em) : 0;  // 0: giant star->path on; 3: off
+  int mapmode = em ? atoi(em) : 3;  // 0: giant star->path on; 3: off
   const char* esl = getenv("SHEEP_KB_SCAN");
   uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
   // counters: [1] n_linked, [4..5] unused queue cursor
@@ -1159,10 +1161,14 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
     hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
                        (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
-    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
+    const char* eq = getenv("SHEEP_KB_QCHUNK");
+    const char* eg = getenv("SHEEP_KB_ZGRID");
+    uint32_t qchunk = eq ? (uint32_t)atoi(eq) : 64;
+    unsigned zgrid = eg ? (unsigned)atoi(eg) : MAX_GRID;
+    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
                        (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap, B1, uf,
                        (const uint32_t*)label, parent, jump, next, st + 8, B0, linked, n_linked,
-                       mapmode == 0 ? 1 : 0, scan_limit);
+                       mapmode == 0 ? 1 : 0, scan_limit, qchunk);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
