@@ -44,7 +44,8 @@ def pmc_traffic(kernel, scale):
     collected for this workload: FETCH_SIZE and WRITE_SIZE from separate rocprofv3 --pmc passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        rec = json.load(open(path))["rmat%d" % scale][kernel]
+        tab = json.load(open(path))["rmat%d" % scale]
+        rec = tab.get(kernel) or tab["sheep::" + kernel]
         return rec["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None

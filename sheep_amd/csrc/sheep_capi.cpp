@@ -227,13 +227,15 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     const char* ek = getenv("SHEEP_KB_BUCKETS");
     const char* er = getenv("SHEEP_KB_RANKB");
     uint32_t K_e = ek ? (uint32_t)atoi(ek) : 64;
-    uint32_t K_r = er ? (uint32_t)atoi(er) : 0;
+    uint32_t K_r = er ? (uint32_t)atoi(er) : 64;
     uint32_t K = K_e + K_r;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
     uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
     uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 64);
     uint32_t* bitmap = (uint32_t*)c.scratch.get("kb_bitmap", ((size_t)n_seq / 32 + 2) * 4);
+    uint32_t* spq = (uint32_t*)c.scratch.get("kb_spq", ((size_t)n_seq / 32 + 64) * 4);
+    (void)hipMemsetAsync(counters, 0, 16, s);
     (void)hipMemsetAsync(bitmap, 0, ((size_t)n_seq / 32 + 2) * 4, s);
     // the sort's free ping-pong buffer holds the kept (b, g) pairs of a bucket
     uint32_t* kept_b = (uint32_t*)spare;
@@ -262,8 +264,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     for (size_t k = 0; k + 1 < bk.size(); ++k) {
       if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
       launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
-                       label, d_parent, jump, kept_b, kept_g, linked, bitmap, counters, stats, ws,
-                       s);
+                       label, d_parent, jump, kept_b, kept_g, linked, bitmap, spq, counters, stats,
+                       ws, s);
       if (per_bucket) {
         unsigned long long h[16];
         HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));

@@ -73,8 +73,8 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* counters, bool stats, unsigned long long* st,
-                      hipStream_t s);
+                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, bool stats,
+                      unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);

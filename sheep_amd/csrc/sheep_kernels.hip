@@ -662,8 +662,16 @@ __device__ __forceinline__ uint32_t ld_parent(uint32_t* p) {
 
 struct ZState {
   uint32_t a, b, x, prev, p;
+  uint32_t flags;  // ZF_* (kb spine mode only)
   bool fresh;
 };
+
+// ZState flags.  ZF_KEEP: the pending edge may carry a marked rank's connection to G — a
+// giant-path edge (G, b) from the spine queue, or any zipper continuation (b, p), which takes
+// over the forest edge (x, p) it displaced — so the redundancy rule below must not drop it
+// (only edges that have not yet changed the forest are dropped).  ZF_SPINE: the walk of the
+// current pending edge has reached the spine (checked once per pending edge).
+constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u;
 
 struct ZCount {
   uint32_t steps = 0, cas = 0, fail = 0;
@@ -676,11 +684,63 @@ struct ZRec {  // where to record pre-bucket roots (x < B0) that a CAS links for
   uint32_t* n_linked = nullptr;
 };
 
-template <int LOAD, int JUMP, bool STATS, bool REC = false>
+// The giant's spine inside a kb bucket [B0, B1).  G is the elimination-tree root of the
+// component of rank B0 - 1 (in a degree-ordered sequence: the giant); bitmap marks the ranks
+// of the bucket that have an edge to G's component.  The ancestors of G in the final etree
+// (its spine) form one chain and contain G and every marked rank.  Two facts follow, both
+// used by zip_step (see k_kb_spine for how the marks become forest edges):
+//   * a walk at a spine vertex x for pending edge (x, b) with b marked can stop: b is
+//     already an etree ancestor of x through other edges, so the edge adds nothing;
+//   * a walk at a spine vertex x may jump to the highest marked y < b: y is an etree
+//     ancestor of x, and any walk may move to an etree ancestor below b (the pending edge
+//     (x, b) and (y, b) give the same threshold connectivity).
+struct SpineInfo {
+  const uint32_t* bitmap = nullptr;
+  uint32_t B0 = 0, B1 = 0, G = INV, limit = 64;
+};
+
+__device__ __forceinline__ bool sp_marked(const SpineInfo& sp, uint32_t v) {
+  return v >= sp.B0 && v < sp.B1 && ((sp.bitmap[v >> 5] >> (v & 31)) & 1u);
+}
+
+// Bits of bitmap word w restricted to ranks [lo, hi).
+__device__ __forceinline__ uint32_t word_in(const uint32_t* bitmap, uint32_t w, uint32_t lo,
+                                            uint32_t hi) {
+  uint32_t bits = bitmap[w];
+  if (w == (lo >> 5)) bits &= ~0u << (lo & 31);
+  if (w == ((hi - 1) >> 5) && (hi & 31)) bits &= ~(~0u << (hi & 31));
+  return bits;
+}
+
+// Highest marked y with x < y < b (scans at most sp.limit words below b's); INV if none.
+__device__ __forceinline__ uint32_t sp_pred(const SpineInfo& sp, uint32_t b, uint32_t x) {
+  uint32_t lo = max(x + 1, sp.B0);
+  if (b <= lo) return INV;
+  uint32_t w = (b - 1) >> 5, wl = lo >> 5;
+  for (uint32_t k = 0; k <= sp.limit; ++k) {
+    uint32_t bits = word_in(sp.bitmap, w, lo, b);
+    if (bits) return (w << 5) + 31 - __clz(bits);
+    if (w == wl) break;
+    --w;
+  }
+  return INV;
+}
+
+template <int LOAD, int JUMP, bool STATS, bool REC = false, bool SPINE = false>
 __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZState& s, ZCount& c,
-                                         const ZRec& rec = ZRec()) {
+                                         const ZRec& rec = ZRec(),
+                                         const SpineInfo& sp = SpineInfo()) {
   if (STATS) c.steps++;
   if (!s.fresh) {
+    if (SPINE && !(s.flags & ZF_SPINE) && (s.x == sp.G || sp_marked(sp, s.x))) {
+      s.flags |= ZF_SPINE;
+      if (!(s.flags & ZF_KEEP) && sp_marked(sp, s.b)) return true;
+      uint32_t y = sp_pred(sp, s.b, s.x);
+      if (y != INV) {
+        s.prev = INV;
+        s.x = y;
+      }
+    }
     if (JUMP) {
       uint32_t j = jump[s.x];
       if (j > s.x && j < s.b) {
@@ -717,14 +777,16 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
   s.b = s.p;
   s.x = s.a;
   s.prev = INV;
+  s.flags = ZF_KEEP;
   return false;
 }
 
-__device__ __forceinline__ void zstart(ZState& s, uint32_t a, uint32_t b) {
+__device__ __forceinline__ void zstart(ZState& s, uint32_t a, uint32_t b, uint32_t flags = 0) {
   s.a = a;
   s.b = b;
   s.x = a;
   s.prev = INV;
+  s.flags = flags;
   s.fresh = false;
 }
 
@@ -761,30 +823,24 @@ __global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint
   flush_stats<STATS>(stats, edges, c, maxsteps);
 }
 
-// Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order from
-// one global counter (one atomic per 512 edges) and every lane that finishes an edge takes
-// the next one at the following step, so a wave never idles behind its slowest lane.
-// Edge source of the queue: packed u64 items (hi << 32 | lo) or two u32 arrays.
-__device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
-                                                 uint32_t G, uint32_t limit);
-
+// Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order and
+// every lane that finishes an edge takes the next one at the following step, so a wave never
+// idles behind its slowest lane.
+// Edge source of the queue: packed u64 items (hi << 32 | lo), or (kb) the spine queue
+// followed by the kept (b, g) pairs of a bucket.
 struct EdgeSrc {
   const uint64_t* items;  // packed (hi << 32 | lo)
   const uint32_t* hi;     // or hi[] / lo[]
   const uint32_t* lo;
-  // kb bucket mode (items == nullptr): indices [0, np) are the giant's path slots (rank
-  // B0 + i, edge (pred, B0 + i) when marked in `bitmap`), then [np, np + nk) the kept pairs.
-  const uint32_t* bitmap = nullptr;
-  uint32_t B0 = 0, G = INV, limit = 64;
+  // kb bucket mode (items == nullptr): indices [0, np) are giant-path edges (G, spq[i]),
+  // then [np, np + nk) the kept pairs.
+  const uint32_t* spq = nullptr;
+  uint32_t G = INV;
   uint64_t np = 0;
-  __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a) const {
+  __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a, uint32_t& fl) const {
+    fl = 0;
     if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; return; }
-    if (i < np) {
-      b = B0 + (uint32_t)i;
-      if ((bitmap[b >> 5] >> (b & 31)) & 1u) a = kb_path_pred(bitmap, B0, b, G, limit);
-      else b = INV, a = 0;
-      return;
-    }
+    if (i < np) { b = spq[i]; a = G; fl = ZF_KEEP; return; }
     i -= np;
     b = hi[i];
     a = (b != INV) ? lo[i] : 0u;
@@ -794,18 +850,18 @@ struct EdgeSrc {
 // Queue chunk (edges per wave refill): all waves sweep the list together, so about
 // nwaves * chunk edges are in flight — the concurrency window that the zipper's rework grows
 // with.  Set per launch by the host (qchunk).
-template <int LOAD, int JUMP, bool STATS, bool REC>
+template <int LOAD, int JUMP, bool STATS, bool REC, bool SPINE = false>
 __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
                                                 uint32_t* parent, uint32_t* jump,
-                                                unsigned long long* next, unsigned long long* stats,
-                                                const ZRec& rec, uint32_t CH = 512) {
+                                                unsigned long long* stats,
+                                                const ZRec& rec, uint32_t CH = 512,
+                                                const SpineInfo& sp = SpineInfo()) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t cbase = 0, cend = 0;  // wave-uniform chunk cursor
   const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   uint64_t chunk_k = 0;
-  (void)next;
   bool active = false, exhausted = false;
   ZState s;
   ZCount c;
@@ -829,10 +885,10 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
       uint64_t avail = cend - cbase;
       if (!active && k < avail) {
         uint64_t idx = cbase + k;
-        uint32_t b, a;
-        src.get(idx, b, a);
+        uint32_t b, a, fl;
+        src.get(idx, b, a, fl);
         if (b != INV) {
-          zstart(s, a, b);
+          zstart(s, a, b, fl);
           active = true;
           if (STATS) { edges++; st0 = c.steps; }
         }
@@ -841,7 +897,7 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
       freem = __ballot(!active);
     }
     if (__ballot(active) == 0) break;
-    if (active && zip_step<LOAD, JUMP, STATS, REC>(parent, jump, s, c, rec)) {
+    if (active && zip_step<LOAD, JUMP, STATS, REC, SPINE>(parent, jump, s, c, rec, sp)) {
       active = false;
       if (STATS) maxsteps = max(maxsteps, c.steps - st0);
     }
@@ -852,8 +908,9 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
 template <int LOAD, int JUMP, bool STATS>
 __global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
                              uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
+  (void)next;
   EdgeSrc src{items, nullptr, nullptr};
-  tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, next, stats, ZRec());
+  tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, stats, ZRec());
 }
 
 
@@ -928,6 +985,13 @@ __device__ __forceinline__ uint32_t uf_find(uint32_t* uf, uint32_t x) {
   }
 }
 
+// find without path compression, for values every thread of a launch asks for (G): a
+// compressing find would have all of them write the same words.
+__device__ __forceinline__ uint32_t uf_find_ro(const uint32_t* uf, uint32_t x) {
+  for (uint32_t p = uf[x]; p != x; p = uf[x]) x = p;
+  return x;
+}
+
 __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v) {
   for (;;) {
     uint32_t ru = uf_find<true>(uf, u), rv = uf_find<true>(uf, v);
@@ -937,64 +1001,18 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v) {
   }
 }
 
-// Zipper insertion that records pre-bucket roots (x < B0) it links for the first time.
-__device__ __forceinline__ void zip_insert_rec(uint32_t* parent, uint32_t* jump, uint32_t a,
-                                               uint32_t b, uint32_t B0, uint32_t* linked,
-                                               uint32_t* n_linked, ZCount& c) {
-  ZState s;
-  zstart(s, a, b);
-  for (;;) {
-    c.steps++;
-    if (!s.fresh) {
-      uint32_t j = jump[s.x];
-      if (j > s.x && j < s.b) {
-        if (s.prev != INV) jump[s.prev] = j;
-        s.prev = s.x;
-        s.x = j;
-        continue;
-      }
-      s.p = ld_parent<0>(&parent[s.x]);
-    }
-    s.fresh = false;
-    if (s.p < s.b) {
-      if (s.prev != INV) jump[s.prev] = s.p;
-      s.prev = s.x;
-      s.x = s.p;
-      continue;
-    }
-    if (s.x != s.a) jump[s.a] = s.x;
-    if (s.p == s.b) return;
-    c.cas++;
-    uint32_t old = atomicCAS(&parent[s.x], s.p, s.b);
-    if (old != s.p) {
-      c.fail++;
-      s.p = old;
-      s.fresh = true;
-      continue;
-    }
-    if (s.p == INV) {
-      if (s.x < B0) linked[atomicAdd(n_linked, 1u)] = s.x;
-      return;
-    }
-    s.a = s.b;
-    s.b = s.p;
-    s.x = s.a;
-    s.prev = INV;
-  }
-}
-
 template <bool STATS>
 __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
                          uint64_t e_end, uint32_t B0, uint32_t* uf,
                          const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
                          uint32_t* bitmap, unsigned long long* stats, int mapmode) {
   // G: the component of the last pre-bucket vertex (in a degree-ordered sequence: the giant).
-  // Its (G, b) pairs go to a rank bitmap and become path edges (k_kb_path), not zipper walks.
-  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find<false>(uf, B0 - 1)] : INV;
+  // Its (G, b) pairs only mark b in the bucket's rank bitmap (k_kb_spine turns the marks into
+  // a path), they are not zipper walks.
+  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find_ro(uf, B0 - 1)] : INV;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  ZCount c;
   uint64_t edges = 0, kept = 0, inb = 0;
   for (uint64_t base = e_begin + wave * 64; base < e_end; base += nwaves * 64) {
     uint64_t idx = base + lane;
@@ -1017,7 +1035,19 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
     }
     if (STATS) { edges += valid; kept += keep; inb += keep && a >= B0; }
     bool giant = keep && g == G;
-    if (giant) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+    // A hub's (G, b) edges span many waves; only the first wave of the run marks b (a wave
+    // whose b continues from the previous item skips when that item maps to G too: its wave
+    // marked, or skipped by the same rule).  Same-word atomics from every wave serialise.
+    uint32_t pb = INV, pg = INV;
+    if (G != INV && base > e_begin && lane == 0) {
+      uint64_t pit = items[base - 1];
+      uint32_t pa = (uint32_t)pit;
+      pb = (uint32_t)(pit >> 32);
+      pg = pa < B0 ? label[uf_find_ro(uf, pa)] : pa;
+    }
+    pb = __builtin_amdgcn_readfirstlane(pb);
+    pg = __builtin_amdgcn_readfirstlane(pg);
+    if (giant && !(b == pb && pg == G)) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
     // kept pairs stay in place (INVALID holes): no shared append cursor
     if (valid) {
       kept_b[idx - e_begin] = (keep && !giant) ? b : INV;
@@ -1026,55 +1056,76 @@ __global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
   }
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
-    atomicAdd(&stats[1], (unsigned long long)c.steps);
-    atomicAdd(&stats[2], (unsigned long long)c.cas);
-    atomicAdd(&stats[3], (unsigned long long)c.fail);
     atomicAdd(&stats[5], (unsigned long long)kept);
     atomicAdd(&stats[6], (unsigned long long)inb);
   }
 }
 
-// Star -> path for the giant G: G is adjacent to the marked ranks b1 < b2 < ... of the bucket.
-// For the etree that star is equivalent to the path G-b1-b2-...: at every threshold both
-// connect G with exactly the marked ranks present.  So a marked b gets the edge
-// (previous marked rank, b) — a walk that starts next to its target — or (G, b) for the first
-// (also when none is found within 64 words back: always valid, only a longer walk).
-__device__ __forceinline__ uint32_t kb_path_pred(const uint32_t* bitmap, uint32_t B0, uint32_t b,
-                                                 uint32_t G, uint32_t limit) {
-  const uint32_t w0 = B0 >> 5, w = b >> 5;
-  uint32_t lo_mask = (w == w0) ? (~0u << (B0 & 31)) : ~0u;
-  uint32_t bits = bitmap[w] & lo_mask & ((1u << (b & 31)) - 1u);
-  if (bits) return (w << 5) + 31 - __clz(bits);
-  for (uint32_t v = w, k = 0; v > w0 && k < limit; --v, ++k) {
-    uint32_t pb = bitmap[v - 1] & ((v - 1 == w0) ? (~0u << (B0 & 31)) : ~0u);
-    if (pb) return ((v - 1) << 5) + 31 - __clz(pb);
+// Star -> path for the giant.  G's edges into the bucket go to the marked ranks b1 < b2 < ...;
+// for the etree that star is equivalent to the path G-b1-b2-...: at every threshold both
+// connect G with exactly the marked ranks present.  The path edges (b_i, b_i+1) are written
+// straight into the forest (parent[] of every in-bucket rank is still INVALID here, so this
+// is what the zipper would do, in one store).  A run of marks is cut where the next mark is
+// more than `limit` words away; each run's first mark b is queued as the edge (G, b), which
+// the zipper inserts (walking G's chain).  One thread per bitmap word; the forward search of
+// a word's last mark and the backward search of a word's first mark are symmetric, so every
+// mark gets exactly one incoming connection.
+__global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
+                           uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit) {
+  const uint32_t w0 = B0 >> 5, w1 = (B1 - 1) >> 5;
+  for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
+       w += gridDim.x * blockDim.x) {
+    uint32_t bits = word_in(bitmap, w, B0, B1);
+    if (!bits) continue;
+    uint32_t cur = (w << 5) + __ffs(bits) - 1;
+    const uint32_t first = cur;
+    bits &= bits - 1;
+    while (bits) {
+      uint32_t nx = (w << 5) + __ffs(bits) - 1;
+      bits &= bits - 1;
+      parent[cur] = nx;
+      cur = nx;
+    }
+    for (uint32_t v = w + 1, k = 0; v <= w1 && k < limit; ++v, ++k) {
+      uint32_t nb = word_in(bitmap, v, B0, B1);
+      if (nb) { parent[cur] = (v << 5) + __ffs(nb) - 1; break; }
+    }
+    bool has_pred = false;
+    for (uint32_t v = w, k = 0; v > w0 && k < limit; --v, ++k)
+      if (word_in(bitmap, v - 1, B0, B1)) { has_pred = true; break; }
+    if (!has_pred) spq[atomicAdd(n_spine, 1u)] = first;
   }
-  return G;
 }
 
-// The kb in-bucket pass: the kept (g, b) list of a bucket (count on the device) through the
-// balanced lane queue, recording pre-bucket roots it links.
+// The kb in-bucket pass: the spine queue, then the kept (b, g) pairs of the bucket, through
+// the balanced lane queue with the spine rules (SpineInfo), recording pre-bucket roots it links.
 template <bool STATS>
 __global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
-                         uint64_t nk, const uint32_t* __restrict__ bitmap, uint32_t B1,
-                         uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
-                         uint32_t* jump, unsigned long long* next, unsigned long long* stats,
-                         uint32_t B0, uint32_t* linked, uint32_t* n_linked, int giant,
-                         uint32_t scan_limit, uint32_t qchunk) {
+                         uint64_t nk, const uint32_t* __restrict__ bitmap,
+                         const uint32_t* __restrict__ spq, const uint32_t* __restrict__ n_spine,
+                         uint32_t B0, uint32_t B1, uint32_t* uf, const uint32_t* __restrict__ label,
+                         uint32_t* parent, uint32_t* jump, unsigned long long* stats,
+                         uint32_t* linked, uint32_t* n_linked, int giant, uint32_t scan_limit,
+                         uint32_t qchunk) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
   EdgeSrc src{nullptr, kb, kg};
+  SpineInfo sp;
   if (giant && B0 > 0) {
-    src.bitmap = bitmap;
-    src.B0 = B0;
-    src.G = label[uf_find<false>(uf, B0 - 1)];
-    src.np = B1 - B0;
-    src.limit = scan_limit;
+    sp.bitmap = bitmap;
+    sp.B0 = B0;
+    sp.B1 = B1;
+    sp.G = label[uf_find_ro(uf, B0 - 1)];
+    sp.limit = scan_limit;
+    src.spq = spq;
+    src.G = sp.G;
+    src.np = *n_spine;
+    tree_queue_body<0, 1, STATS, true, true>(src, src.np + nk, parent, jump, stats, rec, qchunk, sp);
+  } else {
+    tree_queue_body<0, 1, STATS, true, false>(src, nk, parent, jump, stats, rec, qchunk);
   }
-  uint64_t n = src.np + nk;
-  tree_queue_body<0, 1, STATS, true>(src, n, parent, jump, next, stats, rec, qchunk);
 }
 
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
@@ -1095,11 +1146,12 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
   }
 }
 
+// counters[1] = n_linked and counters[2] = n_spine are reset here for the next bucket.
 __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
-                           uint32_t B0, uint32_t B1, uint32_t* n_linked) {
+                           uint32_t B0, uint32_t B1, uint32_t* counters) {
   for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
     if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_linked = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { counters[1] = 0; counters[2] = 0; }
 }
 
 // Bucket boundaries by edge count: thread k finds m_valid (first INVALID hi), takes the rank at
@@ -1141,40 +1193,45 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
                      items, n, K_e, K_r, n_seq, out);
 }
 
+// counters: 4 device words, zero before the first bucket ([1] n_linked, [2] n_spine; each
+// bucket's label kernel resets them).  spq: (n_seq / 32 + 64) words.
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* counters, bool stats,
+                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, bool stats,
                       unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
-  int mapmode = em ? atoi(em) : 3;  // 0: giant star->path on; 3: off
+  int mapmode = em ? atoi(em) : 0;  // 0: giant spine on; 3: off (ablation)
   const char* esl = getenv("SHEEP_KB_SCAN");
   uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
-  // counters: [1] n_linked, [4..5] unused queue cursor
   uint32_t* n_linked = counters + 1;
-  unsigned long long* next = (unsigned long long*)(counters + 4);
-  (void)hipMemsetAsync(counters, 0, 16, s);
+  uint32_t* n_spine = counters + 2;
+  bool giant = mapmode == 0 && B0 > 0;
   if (e_end > e_begin) {
     uint64_t waves = (e_end - e_begin + 63) / 64;
     unsigned grid = grid_for(waves * 64);
     auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
     hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
                        (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
+    if (giant)
+      hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
+                         0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
     const char* eq = getenv("SHEEP_KB_QCHUNK");
     const char* eg = getenv("SHEEP_KB_ZGRID");
     uint32_t qchunk = eq ? (uint32_t)atoi(eq) : 64;
     unsigned zgrid = eg ? (unsigned)atoi(eg) : MAX_GRID;
     hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
-                       (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap, B1, uf,
-                       (const uint32_t*)label, parent, jump, next, st + 8, B0, linked, n_linked,
-                       mapmode == 0 ? 1 : 0, scan_limit, qchunk);
+                       (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap,
+                       (const uint32_t*)spq, (const uint32_t*)n_spine, B0, B1, uf,
+                       (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
+                       giant ? 1 : 0, scan_limit, qchunk);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
-                     (const uint32_t*)parent, uf, label, B0, B1, n_linked);
+                     (const uint32_t*)parent, uf, label, B0, B1, counters);
 }
 
 __global__ void k_iota(uint32_t* p, uint32_t n) {

@@ -222,3 +222,28 @@ def test_sharded_partial_trees_with_degree_pst(oracle, gpu, seed):
     wp, ws = oracle.build_tree(uv, oseq)
     assert np.array_equal(acc[0][:n_seq].cpu().numpy().view(np.uint32), wp)
     assert np.array_equal(acc[1][:n_seq].cpu().numpy().view(np.uint32), ws)
+
+
+KB_KNOBS = [
+    {},                                                    # defaults (giant spine on)
+    {"SHEEP_KB_MAPMODE": "3"},                             # spine off
+    {"SHEEP_KB_SCAN": "1"},                                # runs cut at every gap > 1 word
+    {"SHEEP_KB_SCAN": "0", "SHEEP_KB_BUCKETS": "256"},     # every word its own run
+    {"SHEEP_KB_BUCKETS": "4", "SHEEP_KB_RANKB": "8"},      # few, wide buckets
+    {"SHEEP_KB_BUCKETS": "512", "SHEEP_KB_QCHUNK": "1"},   # many buckets, tiny queue chunks
+    {"SHEEP_TREE_ALGO": "zip"},                            # plain zipper, no buckets
+]
+
+
+@pytest.mark.parametrize("knobs", KB_KNOBS, ids=lambda k: ",".join("%s=%s" % (a[6:], b) for a, b in k.items()) or "default")
+@pytest.mark.parametrize("scale,seed", [(15, 5), (17, 6)])
+def test_tree_knobs_exact(oracle, api, monkeypatch, knobs, scale, seed):
+    """The tree is the same unique etree under every bucketing / spine / queue setting: the
+    knobs change the work, never the result (R-MAT, where a giant component forms)."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    uv = oracle.rmat(scale, 16, seed)
+    seq = oracle.degree_sequence(uv)
+    check_tree(oracle, api, uv, seq)
+    rng = np.random.default_rng(seed)
+    check_tree(oracle, api, uv, rng.permutation(seq).astype(np.uint32))  # no giant at the end
