@@ -399,16 +399,33 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
 }
 
 // ---------------------------------------------------------------------------------------
-// Stable LSD radix sort of packed u64 items (key = upper 32 bits), 8-bit digits.
-// Tile = 1024 threads x 8 items.  Per pass: k_rsort_count (tile digit histograms, digit-major
-// matrix) -> exclusive scan -> k_rsort_scatter: the tile is ranked stably in LDS (64-lane
-// ballot match per chunk, per-wave digit counts), staged in LDS in digit order, and written
-// out so that consecutive lanes store consecutive addresses of one digit run.
+// Stable LSD radix sort of packed u64 items (key = upper 32 bits), 8- or 9-bit digits.
+// Tile = 1024 threads x 8 items; wave w owns tile items [512 w, 512 w + 512), read in 8
+// rounds of 64 consecutive items (coalesced).  Per pass: k_rsort_count (tile digit
+// histograms, digit-major matrix) -> exclusive scan -> k_rsort_scatter.
+// Ranking is wave-private: in each round the lanes holding one digit find each other with a
+// ballot match, and a per-wave LDS counter per digit gives the stable rank inside the wave —
+// no block barrier per round.  Then one pass over the digits turns the per-wave counts into
+// per-wave offsets, the tile is staged in LDS in digit order, and written so that
+// consecutive lanes store consecutive addresses of one digit run.
 // ---------------------------------------------------------------------------------------
 static constexpr int RS_THREADS = 1024;
 static constexpr int RS_ITEMS = 8;
 static constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 static constexpr int RS_WAVES = RS_THREADS / 64;
+
+// Lanes of the wave (among `valid` ones) whose digit equals this lane's d.
+template <int DB>
+__device__ __forceinline__ uint64_t digit_match(uint32_t d, bool valid) {
+  uint64_t match = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < DB; ++b) {
+    bool bit = (d >> b) & 1u;
+    uint64_t bal = __ballot(bit);
+    match &= bit ? bal : ~bal;
+  }
+  return match;
+}
 
 template <int DB>  // digit bits: 8 or 9
 __global__ void __launch_bounds__(RS_THREADS)
@@ -416,16 +433,26 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
               uint32_t ntiles) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint32_t hist[NBIN];
-  for (uint32_t i = threadIdx.x; i < NBIN; i += RS_THREADS) hist[i] = 0;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS) hist[i] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (64 * RS_ITEMS) + lane;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t it[RS_ITEMS];
 #pragma unroll
-  for (int i = 0; i < RS_ITEMS; ++i) {
-    uint64_t idx = base + (uint64_t)i * RS_THREADS + threadIdx.x;
-    if (idx < n) atomicAdd(&hist[(uint32_t)(in[idx] >> (32 + shift)) & (NBIN - 1)], 1u);
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    uint64_t idx = base + (uint64_t)k * 64;
+    it[k] = idx < n ? in[idx] : 0ull;
+  }
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    bool valid = base + (uint64_t)k * 64 < n;
+    uint32_t d = (uint32_t)(it[k] >> (32 + shift)) & (NBIN - 1);
+    uint64_t match = digit_match<DB>(d, valid);  // one LDS add per distinct digit (skewed keys)
+    if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < NBIN; i += RS_THREADS)
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS)
     counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
@@ -436,70 +463,57 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint64_t stage[RS_TILE];
   __shared__ uint32_t whist[RS_WAVES][NBIN];
-  __shared__ uint32_t tstart[NBIN], running[NBIN], goff[NBIN], wsum[RS_WAVES];
+  __shared__ uint32_t tstart[NBIN], goff[NBIN], wsum[RS_WAVES];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
-  const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)RS_TILE ? (n - base) : RS_TILE);
+  const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
+  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : RS_TILE);
+  const uint32_t wbase = (uint32_t)w * (64 * RS_ITEMS) + lane;  // tile index of round 0
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS) goff[i] = offsets[(uint64_t)i * ntiles + blockIdx.x];
+  for (uint32_t i = lane; i < NBIN; i += 64) whist[w][i] = 0;
   uint64_t item[RS_ITEMS];
-  uint32_t dg[RS_ITEMS];
-  for (uint32_t i = t; i < NBIN; i += RS_THREADS) {
-    running[i] = 0;
-    goff[i] = offsets[(uint64_t)i * ntiles + blockIdx.x];
-  }
-  for (int i = t; i < RS_WAVES * (int)NBIN; i += RS_THREADS) (&whist[0][0])[i] = 0;
+  uint32_t rk[RS_ITEMS];
 #pragma unroll
-  for (int i = 0; i < RS_ITEMS; ++i) {
-    uint32_t li = (uint32_t)i * RS_THREADS + t;
-    item[i] = li < tile_n ? in[base + li] : 0ull;
-    dg[i] = (uint32_t)(item[i] >> (32 + shift)) & (NBIN - 1);
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    uint32_t li = wbase + (uint32_t)k * 64;
+    item[k] = li < tile_n ? in[tbase + li] : 0ull;
+  }
+  // stable rank inside the wave: rounds in item order, lanes in item order within a round
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    bool valid = wbase + (uint32_t)k * 64 < tile_n;
+    uint32_t d = (uint32_t)(item[k] >> (32 + shift)) & (NBIN - 1);
+    uint64_t match = digit_match<DB>(d, valid);
+    uint32_t before = (uint32_t)__popcll(match & lt);
+    uint32_t prev = whist[w][d];
+    rk[k] = prev + before;
+    if (valid && before == 0) whist[w][d] = prev + (uint32_t)__popcll(match);
   }
   __syncthreads();
-  // tile digit totals -> tstart (exclusive); whist[0] doubles as the histogram
-  for (int i = 0; i < RS_ITEMS; ++i)
-    if ((uint32_t)i * RS_THREADS + t < tile_n) atomicAdd(&whist[0][dg[i]], 1u);
-  __syncthreads();
-  if (t < (int)NBIN) {
-    uint32_t v = whist[0][t];
-    uint32_t incl = wave_incl_scan(v);
+  // per-wave counts -> per-wave exclusive offsets inside each digit; tile digit totals -> tstart
+  for (uint32_t dd = t; dd < NBIN; dd += RS_THREADS) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < RS_WAVES; ++i) { uint32_t v = whist[i][dd]; whist[i][dd] = s; s += v; }
+    uint32_t incl = wave_incl_scan(s);
     if (lane == 63) wsum[w] = incl;
-    tstart[t] = incl - v;
+    tstart[dd] = incl - s;
   }
   __syncthreads();
   if (t < (int)NBIN) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
-    whist[0][t] = 0;
   }
   __syncthreads();
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
-  for (int c = 0; c < RS_ITEMS; ++c) {
-    bool valid = (uint32_t)c * RS_THREADS + t < tile_n;
-    uint32_t d = dg[c];
-    uint64_t match = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < DB; ++b) {
-      bool bit = (d >> b) & 1u;
-      uint64_t bal = __ballot(bit);
-      match &= bit ? bal : ~bal;
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    if (wbase + (uint32_t)k * 64 < tile_n) {
+      uint32_t d = (uint32_t)(item[k] >> (32 + shift)) & (NBIN - 1);
+      stage[tstart[d] + whist[w][d] + rk[k]] = item[k];
     }
-    uint32_t before = (uint32_t)__popcll(match & lt);
-    if (valid && before == 0) whist[w][d] = (uint32_t)__popcll(match);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = tstart[d] + running[d] + before;
-      for (int i = 0; i < w; ++i) pos += whist[i][d];
-      stage[pos] = item[c];
-    }
-    __syncthreads();
-    for (uint32_t dd = t; dd < NBIN; dd += RS_THREADS) {
-      uint32_t tot = 0;
-      for (int i = 0; i < RS_WAVES; ++i) { tot += whist[i][dd]; whist[i][dd] = 0; }
-      running[dd] += tot;
-    }
-    __syncthreads();
   }
+  __syncthreads();
   for (uint32_t j = t; j < tile_n; j += RS_THREADS) {
     uint64_t it = stage[j];
     uint32_t d = (uint32_t)(it >> (32 + shift)) & (NBIN - 1);
