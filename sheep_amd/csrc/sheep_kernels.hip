@@ -232,33 +232,46 @@ void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32
 // ---------------------------------------------------------------------------------------
 // Bucketed degree histogram (the path for large m).  Random global atomics run at ~22 G/s on
 // MI355X (k_degree above: 95 ms for RMAT-26's 2.1 G endpoints), so endpoints are first
-// partitioned by id range into NB <= 2048 buckets of 2^SH <= 32768 ids (one LDS-resident
-// counter slice each), then counted in LDS:
+// partitioned by id range into NB <= 1024 buckets of 2^SH <= 65536 ids, written as 16-bit
+// local ids, then counted in LDS:
 //   k_degb_count    per-chunk bucket counts -> counts[bucket][chunk] (digit-major, scanned)
-//   k_degb_scatter  block-local counting sort in LDS, then each wave writes whole bucket runs:
-//                   entries are 16-bit (local id | self-loop flag << 15)
-//   k_degb_hist     one workgroup per bucket: LDS counters, wave-level aggregation of repeated
-//                   ids (hubs), coalesced write of the degree slice
-// LLAMA mode emits t, and h only when t != h; FILE mode emits both.  A self-loop record is
-// flagged once, so selfc[v] = number of self-loop records at v.
+//   k_degb_scatter  block-local counting sort of the chunk in LDS (its counts come from
+//                   k_degb_count), then each wave writes whole bucket runs (~128 B at RMAT-26);
+//                   self-loop records also bump selfc[v] (global atomics: self-loops are rare)
+//   k_degb_hist     one workgroup per (bucket, half of its id range <= 32768 ids): LDS
+//                   counters, wave-level aggregation of repeated ids (hubs), coalesced write
+// LLAMA mode emits t, and h only when t != h; FILE mode emits both.
+// Supports n_ids <= 2^26 (launch_degree_bucketed falls back to k_degree above that).
 // ---------------------------------------------------------------------------------------
 static constexpr int DEGB_THREADS = 1024;
 static constexpr int DEGB_CHUNK = 32768;  // edges per chunk (<= 65536 endpoints -> 128 KB LDS)
+static constexpr uint32_t DEGB_NB = 1024;
+static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgroup
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
              uint32_t NB, uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t* err) {
-  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t hist[DEGB_NB];
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
-  for (int i = 0; i < DEGB_CHUNK / DEGB_THREADS; ++i) {
-    uint64_t idx = base + (uint64_t)i * DEGB_THREADS + threadIdx.x;
-    if (idx >= m) break;
-    uint2 e = uv[idx];
-    if (e.x >= n_ids || e.y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
-    atomicAdd(&hist[e.x >> SH], 1u);
-    if (file_mode || e.x != e.y) atomicAdd(&hist[e.y >> SH], 1u);
+  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
+  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
+  constexpr int U = 8;  // records loaded per thread before use (bytes in flight)
+  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {
+    uint2 e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + threadIdx.x;
+      e[u] = i < cn ? uv[base + i] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + threadIdx.x;
+      if (i >= cn) continue;
+      if (e[u].x >= n_ids || e[u].y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
+      atomicAdd(&hist[e[u].x >> SH], 1u);
+      if (file_mode || e[u].x != e[u].y) atomicAdd(&hist[e[u].y >> SH], 1u);
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x)
@@ -267,109 +280,132 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
-               uint32_t NB, const uint32_t* __restrict__ offsets, uint32_t nchunks,
-               uint16_t* __restrict__ ep) {
-  __shared__ uint32_t hist[2048];
-  __shared__ uint32_t start[2048];
+               uint32_t NB, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
+               uint32_t nchunks, uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc) {
+  __shared__ uint32_t cur[DEGB_NB], start[DEGB_NB], goff[DEGB_NB], wsum[DEGB_THREADS / 64];
   __shared__ uint16_t buf[2 * DEGB_CHUNK];
-  __shared__ uint32_t wsum[DEGB_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t lmask = (1u << SH) - 1u;
-  for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
+  // this chunk's bucket counts and global run offsets (one scattered read per thread)
+  uint32_t cnt = 0;
+  if (t < (int)NB) {
+    cnt = counts[(uint64_t)t * nchunks + blockIdx.x];
+    goff[t] = offsets[(uint64_t)t * nchunks + blockIdx.x];
+  }
+  uint32_t incl = wave_incl_scan(cnt);
+  if (lane == 63) wsum[w] = incl;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
-  for (int i = 0; i < DEGB_CHUNK / DEGB_THREADS; ++i) {
-    uint64_t idx = base + (uint64_t)i * DEGB_THREADS + threadIdx.x;
-    if (idx >= m) break;
-    uint2 e = uv[idx];
-    if (e.x >= n_ids || e.y >= n_ids) continue;
-    atomicAdd(&hist[e.x >> SH], 1u);
-    if (file_mode || e.x != e.y) atomicAdd(&hist[e.y >> SH], 1u);
+  if (t < (int)NB) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    start[t] = add + incl - cnt;
+    cur[t] = add + incl - cnt;
   }
   __syncthreads();
-  // exclusive scan of hist[0..NB) -> start (2 items per thread; NB <= 2048)
-  {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t a0 = (2 * t < (int)NB) ? hist[2 * t] : 0, a1 = (2 * t + 1 < (int)NB) ? hist[2 * t + 1] : 0;
-    uint32_t incl = wave_incl_scan(a0 + a1);
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t wb = 0;
-    for (int i = 0; i < w; ++i) wb += wsum[i];
-    uint32_t ex = wb + incl - a0 - a1;
-    if (2 * t < (int)NB) start[2 * t] = ex;
-    if (2 * t + 1 < (int)NB) start[2 * t + 1] = ex + a0;
+  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
+  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
+  constexpr int U = 8;
+  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {
+    uint2 ee[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + t;
+      ee[u] = i < cn ? uv[base + i] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + t;
+      uint2 e = ee[u];
+      if (i >= cn || e.x >= n_ids || e.y >= n_ids) continue;
+      bool loop = e.x == e.y;
+      buf[atomicAdd(&cur[e.x >> SH], 1u)] = (uint16_t)(e.x & lmask);
+      if (file_mode || !loop) buf[atomicAdd(&cur[e.y >> SH], 1u)] = (uint16_t)(e.y & lmask);
+      if (loop && selfc) atomicAdd(&selfc[e.x], 1u);
+    }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = start[i];  // hist := cursor
-  __syncthreads();
-  for (int i = 0; i < DEGB_CHUNK / DEGB_THREADS; ++i) {
-    uint64_t idx = base + (uint64_t)i * DEGB_THREADS + threadIdx.x;
-    if (idx >= m) break;
-    uint2 e = uv[idx];
-    if (e.x >= n_ids || e.y >= n_ids) continue;
-    bool loop = e.x == e.y;
-    buf[atomicAdd(&hist[e.x >> SH], 1u)] = (uint16_t)((e.x & lmask) | (loop ? 0x8000u : 0u));
-    if (file_mode || !loop) buf[atomicAdd(&hist[e.y >> SH], 1u)] = (uint16_t)(e.y & lmask);
-  }
-  __syncthreads();
-  // hist[b] is now the end of bucket b's run in buf; each wave writes whole runs
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // each wave writes whole bucket runs
   for (uint32_t b = w; b < NB; b += DEGB_THREADS / 64) {
-    uint32_t s0 = start[b], n = hist[b] - s0;
-    uint64_t g = offsets[(uint64_t)b * nchunks + blockIdx.x];
+    uint32_t s0 = start[b], n = cur[b] - s0;
+    uint64_t g = goff[b];
     for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];
   }
 }
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
-            const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t n_ids,
-            uint32_t* __restrict__ deg, uint32_t* __restrict__ selfc) {
-  __shared__ uint32_t cnt[32768];
-  const uint32_t b = blockIdx.x, span = 1u << SH;
+            const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
+            uint32_t n_ids, uint32_t* __restrict__ deg) {
+  __shared__ uint32_t cnt[DEGB_HALF];
+  const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
+  const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
   uint64_t s0 = offsets[(uint64_t)b * nchunks];
   const uint64_t last = (uint64_t)NB * nchunks - 1;
   uint64_t s1 = (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks] : (uint64_t)offsets[last] + counts[last];
   const int lane = threadIdx.x & 63;
-  for (uint64_t i0 = s0; i0 < s1; i0 += DEGB_THREADS) {
-    uint64_t i = i0 + threadIdx.x;
-    bool valid = i < s1;
-    uint32_t e = valid ? ep[i] : 0u;
-    uint32_t v = e & 0x7FFFu;
-    if (valid && (e & 0x8000u) && selfc) atomicAdd(&selfc[((uint64_t)b << SH) + v], 1u);
-    bool done = !valid;
-    // two rounds of leader matching fold a hub's repeated id into one LDS add
-    for (int r = 0; r < 2; ++r) {
-      uint64_t act = __ballot(!done);
-      if (!act) break;
-      int leader = __ffsll((unsigned long long)act) - 1;
-      uint32_t lv = __builtin_amdgcn_readlane(v, leader);
-      uint64_t same = __ballot(!done && v == lv);
-      if (lane == leader) atomicAdd(&cnt[lv], (uint32_t)__popcll(same));
-      if ((same >> lane) & 1) done = true;
+  // 32 entries (four 16-B loads, all issued before use: the loop is latency-bound otherwise)
+  // per thread per iteration, from the 8-aligned entry below s0 (ep is padded: the loads may
+  // run up to 7 entries past the end)
+  constexpr int V = 4;
+  for (uint64_t i0 = s0 & ~7ull; i0 < s1; i0 += 8 * V * DEGB_THREADS) {
+    uint4 q[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
+      q[u] = i < s1 ? *(const uint4*)(ep + i) : make_uint4(0, 0, 0, 0);
     }
-    if (!done) atomicAdd(&cnt[v], 1u);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
+      uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint64_t ik = i + k;
+        uint32_t e = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        bool done = !(ik >= s0 && ik < s1) || (H > 1 && (e >> 15) != h);
+        uint32_t v = H > 1 ? (e & (DEGB_HALF - 1)) : e;
+        // one round of leader matching folds a hub's repeated id into one LDS add
+        uint64_t act = __ballot(!done);
+        if (act) {
+          int leader = __ffsll((unsigned long long)act) - 1;
+          uint32_t lv = __builtin_amdgcn_readlane(v, leader);
+          uint64_t same = __ballot(!done && v == lv);
+          if (lane == leader) atomicAdd(&cnt[lv], (uint32_t)__popcll(same));
+          if ((same >> lane) & 1) done = true;
+          if (!done) atomicAdd(&cnt[v], 1u);
+        }
+      }
+    }
   }
   __syncthreads();
-  uint64_t g0 = (uint64_t)b << SH;
+  uint64_t g0 = ((uint64_t)b << SH) + (uint64_t)h * span;
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x)
     if (g0 + i < n_ids) deg[g0 + i] = cnt[i];
 }
 
-size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
+// SH: local-id bits, NB buckets; false when n_ids is beyond the bucketed path (> 2^26).
+static bool degb_params(uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
   int bits = 0;
   for (uint64_t v = n_ids ? n_ids - 1 : 0; v; v >>= 1) ++bits;
-  int SH = bits - 11;
+  int SH = bits - 10;
   if (SH < 0) SH = 0;
-  if (SH > 15) SH = 15;
-  uint32_t NB = (uint32_t)(((uint64_t)n_ids + (1u << SH) - 1) >> SH);
+  if (SH > 16) return false;
+  *SH_out = SH;
+  *NB_out = (uint32_t)(((uint64_t)n_ids + (1u << SH) - 1) >> SH);
+  return true;
+}
+
+size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
+  int SH = 0;
+  uint32_t NB = 0;
+  if (!degb_params(n_ids, &SH, &NB)) return 1;
   uint64_t nchunks = (m + DEGB_CHUNK - 1) / DEGB_CHUNK;
   if (SH_out) *SH_out = SH;
   if (NB_out) *NB_out = NB;
   uint64_t cw = (uint64_t)NB * nchunks;
-  return 2 * cw + scan_tmp_words(cw) + (2 * m + 1) / 2 + 1;  // counts, offsets, scan tmp, u16 ep
+  return 2 * cw + scan_tmp_words(cw) + (2 * m + 1) / 2 + 16;  // counts, offsets, scan tmp, u16 ep (+pad)
 }
 
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
@@ -378,7 +414,10 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                             hipStream_t s) {
   int SH;
   uint32_t NB;
-  degb_tmp_words(m, n_ids, &SH, &NB);
+  if (!degb_params(n_ids, &SH, &NB)) {
+    launch_degree(uv, m, n_ids, file_mode, deg, selfc, err, s);
+    return;
+  }
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (n_ids == 0) return;
   if (m == 0) { (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s); return; }
@@ -387,15 +426,17 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   uint32_t* counts = tmp;
   uint32_t* offsets = tmp + cw;
   uint32_t* stmp = offsets + cw;
-  uint16_t* ep = (uint16_t*)(stmp + scan_tmp_words(cw));
+  uint16_t* ep = (uint16_t*)(((uintptr_t)(stmp + scan_tmp_words(cw)) + 15) & ~(uintptr_t)15);
+  uint32_t H = SH > 15 ? 2u : 1u;
   hipLaunchKernelGGL(k_degb_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, counts, nchunks, err);
   launch_scan_exclusive(counts, offsets, cw, stmp, s);
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
-                     n_ids, file_mode, SH, NB, (const uint32_t*)offsets, nchunks, ep);
-  hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
-                     (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, n_ids,
-                     deg, selfc);
+                     n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
+                     nchunks, ep, selfc);
+  hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                     (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
+                     deg);
 }
 
 // ---------------------------------------------------------------------------------------
