@@ -1,3 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python scripts/lab/sort_lab.py 26 > gpurun_out/sort_lab.log 2>&1
+export TMPDIR=/tmp
+export LAB_STATS=1
+SCALE=26 timeout -k 10 300 bash scripts/lab_env.sh "SHEEP_KB_MAPMODE=0:kb:64" "SHEEP_KB_MAPMODE=1:kb:64" > gpurun_out/lab_mm.log 2>&1

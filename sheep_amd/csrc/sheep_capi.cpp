@@ -198,25 +198,29 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
   if (tm) tm->mark("tree_init");
-  launch_edge_pass(d_uv, m, d_rank, n_rank, di ? nullptr : d_pst, items, c.d_err, s);
-  if (tm) tm->mark("edge_pass");
   const char* ea = getenv("SHEEP_TREE_ALGO");
   bool kb = !(ea && strcmp(ea, "zip") == 0);
   const char* es = getenv("SHEEP_TREE_STATS");
   bool stats = es && (es[0] == '1' || es[0] == '2');
+  // Sort keys: hi's bits [lo_bit, top + 1) — bit `top` puts INVALID his after every rank.
+  // kb needs hi order only down to groups of 2^lo_bit ranks (bucket ranges; wave dedupe and
+  // the run lengths that pst needs are done per group inside k_kb_map): 18 bits = 2 passes.
+  // The plain zipper only needs the top 16 bits (order affects work, never the result).
   int top = bits_for(n_seq);
-  // kb needs edges fully sorted by hi (bucket ranges + wave dedupe); the plain zipper only
-  // needs them bucketed by the top 16 bits (order affects work, never the result).
-  // (pst from degrees also needs the full sort: it counts each hi's run.)
-  int lo_bit = (kb || di) ? 0 : std::max(0, top - 16);
-  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top, tmp, s);
+  int lo_bit = std::max(0, top + 1 - (kb ? 18 : 16));
+  // pst from degrees (di) needs the run length of every hi: counted by k_kb_map.  Otherwise
+  // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
+  bool pst_count = kb && di;
+  launch_edge_pass_tiles(d_uv, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
+                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s);
+  if (tm) tm->mark("edge_pass");
+  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
   uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
   if (tm) tm->mark("bucket_sort");
-  if (di) {
-    uint32_t* rs = (uint32_t*)c.scratch.get("pst_start", (size_t)n_seq * 4);
-    uint32_t* re = (uint32_t*)c.scratch.get("pst_end", (size_t)n_seq * 4);
-    launch_pst_from_degree(sorted, m, di->seq, n_seq, di->deg, di->selfc, di->mode, rs, re, d_pst, s);
-    if (tm) tm->mark("pst");
+  uint32_t* hcnt = nullptr;
+  if (pst_count) {
+    hcnt = (uint32_t*)c.scratch.get("hi_count", (size_t)n_seq * 4);
+    launch_fill(hcnt, 0, n_seq, s);
   }
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   if (!kb) {
@@ -245,7 +249,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_iota(uf, n_seq, s);
     launch_iota(label, n_seq, s);
     (void)hipMemsetAsync(ws, 0, 64 * 2, s);
-    launch_kb_bounds(sorted, m, K_e, K_r, n_seq, bounds, s);
+    launch_kb_bounds(sorted, m, K_e, K_r, n_seq, lo_bit, bounds, s);
     std::vector<unsigned long long> hb(2 * (K + 1));
     HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -264,8 +268,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     for (size_t k = 0; k + 1 < bk.size(); ++k) {
       if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
       launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
-                       label, d_parent, jump, kept_b, kept_g, linked, bitmap, spq, counters, stats,
-                       ws, s);
+                       label, d_parent, jump, kept_b, kept_g, linked, bitmap, spq, counters,
+                       lo_bit, hcnt, stats, ws, s);
       if (per_bucket) {
         unsigned long long h[16];
         HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
@@ -276,6 +280,10 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     }
   }
   if (tm) tm->mark("tree_insert");
+  if (pst_count) {
+    launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s);
+    if (tm) tm->mark("pst");
+  }
   if (stats) {
     unsigned long long h[16];
     HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));

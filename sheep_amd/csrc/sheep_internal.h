@@ -54,8 +54,9 @@ size_t scan_tmp_words(uint64_t n);
 void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp,
                            hipStream_t s);
 size_t rsort_tmp_words(uint64_t n);
+int rsort_first_width(int bits);
 uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
-                         int bit_hi, uint32_t* tmp, hipStream_t s);
+                         int bit_hi, uint32_t* tmp, hipStream_t s, bool counted0 = false);
 void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s);
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
                        uint32_t* rank, hipStream_t s);
@@ -65,15 +66,23 @@ void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, ui
 void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                       uint32_t* pst /* nullable: no pst */, uint64_t* items, uint32_t* err,
                       hipStream_t s);
+// edge pass + the first radix pass's tile histograms (sort bits from `shift`, DB wide)
+void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                            uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
+                            uint32_t* tmp, hipStream_t s);
+void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
+                           const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
+                           hipStream_t s);
 // variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
 void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
                         int variant, bool stats, unsigned long long* ws, hipStream_t s);
 void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
-                      uint32_t n_seq, unsigned long long* out, hipStream_t s);
+                      uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s);
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, bool stats,
+                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, int gshift,
+                      uint32_t* cnt /* nullable: hi run lengths */, bool stats,
                       unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,

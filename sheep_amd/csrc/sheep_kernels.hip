@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "rmat.h"
 #include "sheep_internal.h"
 
@@ -86,6 +88,24 @@ __global__ void k_pst_from_degree(const uint32_t* __restrict__ seq, uint32_t n_s
     uint32_t v = seq[r];
     pst[r] = deg[v] - w * selfc[v] - (end[r] - start[r]);
   }
+}
+
+// pst[r] = nsdeg[seq[r]] - cnt[r], cnt[r] = |{records with hi == r}| (counted by k_kb_map).
+__global__ void k_pst_from_count(const uint32_t* __restrict__ seq, uint32_t n_seq,
+                                 const uint32_t* __restrict__ deg, const uint32_t* __restrict__ selfc,
+                                 uint32_t w, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ pst) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_seq; r += gridDim.x * blockDim.x) {
+    uint32_t v = seq[r];
+    pst[r] = deg[v] - w * selfc[v] - cnt[r];
+  }
+}
+
+void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
+                           const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
+                           hipStream_t s) {
+  if (n_seq == 0) return;
+  hipLaunchKernelGGL(k_pst_from_count, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, seq, n_seq, deg,
+                     selfc, file_mode ? 2u : 1u, cnt, pst);
 }
 
 void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* seq, uint32_t n_seq,
@@ -567,30 +587,39 @@ size_t rsort_tmp_words(uint64_t n) {
   return 512 * nt + scan_tmp_words(512 * nt);
 }
 
-// Sorts n items on bits [bit_lo, bit_hi) of their upper word with passes of <= 9 bits (25 bits
-// -> 9+8+8); returns the buffer holding the result (in, a or b).  `in` is never written.
+// Digit width of the first pass when `bits` are sorted in passes of <= 9 bits (even split,
+// wider first): 25 bits -> 9+8+8, 18 -> 9+9.
+int rsort_first_width(int bits) {
+  if (bits <= 0) return 0;
+  int passes = (bits + 8) / 9;
+  return bits / passes + (bits % passes ? 1 : 0);
+}
+
+// Sorts n items on bits [bit_lo, bit_hi) of their upper word with passes of <= 9 bits;
+// returns the buffer holding the result (in, a or b).  `in` is only read by the first pass.
+// counted0: the first pass's tile histograms are already in tmp (k_edge_pass_tiles).
 uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
-                         int bit_hi, uint32_t* tmp, hipStream_t s) {
+                         int bit_hi, uint32_t* tmp, hipStream_t s, bool counted0) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   uint32_t* stmp = tmp + 512 * nt;
   const uint64_t* src = in;
   uint64_t* dst = a;
-  int bits = bit_hi - bit_lo;
-  int passes = bits > 0 ? (bits + 8) / 9 : 0;
-  for (int p = 0, shift = bit_lo; p < passes; ++p) {
-    int width = (bits - (shift - bit_lo)) / (passes - p);          // even split, wider first
-    if ((bits - (shift - bit_lo)) % (passes - p)) width += 1;
+  for (int shift = bit_lo, p = 0; shift < bit_hi; ++p) {
+    int width = rsort_first_width(bit_hi - shift);
     if (n) {
+      bool count = !(p == 0 && counted0);
       if (width > 8) {
-        hipLaunchKernelGGL(k_rsort_count<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
-                           shift, counts, (uint32_t)nt);
+        if (count)
+          hipLaunchKernelGGL(k_rsort_count<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+                             shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
                            n, shift, (const uint32_t*)counts, (uint32_t)nt);
       } else {
-        hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
-                           shift, counts, (uint32_t)nt);
+        if (count)
+          hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+                             shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
                            n, shift, (const uint32_t*)counts, (uint32_t)nt);
@@ -684,6 +713,76 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
   if (m == 0) return;
   hipLaunchKernelGGL(k_edge_pass, dim3(grid_for(m)), dim3(BLOCK), 0, s, (const uint2*)uv, m, rank,
                      n_rank, pst, items, err);
+}
+
+// The edge pass fused with the first radix pass's tile histograms (digit = bits
+// [shift, shift + DB) of hi): one block per RS_TILE records, wave-striped like
+// k_rsort_count; each thread loads its 8 records and issues their 16 rank gathers before using
+// any (the pass is bound by the random gathers: keep many in flight).  pst (nullable) as in
+// k_edge_pass.
+template <int DB>
+__global__ void __launch_bounds__(RS_THREADS)
+k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
+                  uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
+                  uint32_t* err, int shift, uint32_t* __restrict__ counts, uint32_t ntiles) {
+  constexpr uint32_t NBIN = 1u << DB;
+  __shared__ uint32_t hist[NBIN];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS) hist[i] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (64 * RS_ITEMS) + lane;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint2 e[RS_ITEMS];
+  uint32_t rx[RS_ITEMS], ry[RS_ITEMS];
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    uint64_t idx = base + (uint64_t)k * 64;
+    e[k] = idx < m ? uv[idx] : make_uint2(0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    bool g = e[k].x != e[k].y;  // self-loops (and padding) gather nothing
+    rx[k] = (g && e[k].x < n_rank) ? rank[e[k].x] : INV;
+    ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    uint64_t idx = base + (uint64_t)k * 64;
+    bool valid = idx < m;
+    uint32_t hi = INV, lo = INV;
+    if (valid && e[k].x != e[k].y) {
+      bool ox = e[k].x >= n_rank, oy = e[k].y >= n_rank;
+      if ((ox && ry[k] != INV) || (oy && rx[k] != INV)) {
+        atomicOr(err, ERR_RANGE);
+      } else {
+        lo = min(rx[k], ry[k]);
+        hi = max(rx[k], ry[k]);
+        if (lo != INV && pst) atomicAdd(&pst[lo], 1u);
+      }
+    }
+    if (valid) items[idx] = ((uint64_t)hi << 32) | lo;
+    uint32_t d = (hi >> shift) & (NBIN - 1);
+    uint64_t match = digit_match<DB>(d, valid);
+    if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS)
+    counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
+}
+
+// Edge pass whose output feeds radix_sort_u64(..., bit_lo = shift, counted0 = true): tmp is
+// that sort's tmp (rsort_tmp_words(m)); DB = rsort_first_width of the sorted bit range.
+void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                            uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
+                            uint32_t* tmp, hipStream_t s) {
+  if (m == 0) return;
+  uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
+  if (DB > 8)
+    hipLaunchKernelGGL(k_edge_pass_tiles<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s,
+                       (const uint2*)uv, m, rank, n_rank, pst, items, err, shift, tmp, (uint32_t)nt);
+  else
+    hipLaunchKernelGGL(k_edge_pass_tiles<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s,
+                       (const uint2*)uv, m, rank, n_rank, pst, items, err, shift, tmp, (uint32_t)nt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1056,58 +1155,92 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v) {
   }
 }
 
+// The kb map pass over one bucket's records (sorted by hi down to groups of 2^gshift ranks,
+// in stream order inside a group).  Per record (b = hi, a = lo):
+//   g = a (a >= B0) or label[find(a)] (a < B0: a's pre-bucket etree root, exact);
+//   g == G (the giant, see SpineInfo): b is marked in the bucket's rank bitmap;
+//   otherwise (g, b) is kept for the zipper;
+//   cnt[b] += 1 (nullable: the run length of b that pst needs).
+// A block takes chunks of KM_CHUNK records; marks and counts of ranks within KM_WIN of the
+// chunk's first group go to LDS (bitmap + packed 16-bit counts) and reach global memory once
+// per word per chunk — a hub's records span many waves, and same-word atomics from every
+// wave serialise.  Ranks beyond the window use global atomics directly.
+static constexpr int KM_THREADS = 1024;
+static constexpr int KM_CHUNK = 8192;       // < 65536: the packed 16-bit counts cannot carry
+static constexpr uint32_t KM_WIN = 32768;   // ranks
+
 template <bool STATS>
-__global__ void k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin,
-                         uint64_t e_end, uint32_t B0, uint32_t* uf,
-                         const uint32_t* __restrict__ label, uint32_t* kept_b, uint32_t* kept_g,
-                         uint32_t* bitmap, unsigned long long* stats, int mapmode) {
-  // G: the component of the last pre-bucket vertex (in a degree-ordered sequence: the giant).
-  // Its (G, b) pairs only mark b in the bucket's rank bitmap (k_kb_spine turns the marks into
-  // a path), they are not zipper walks.
-  const uint32_t G = (B0 > 0 && mapmode == 0) ? label[uf_find_ro(uf, B0 - 1)] : INV;
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+__global__ void __launch_bounds__(KM_THREADS)
+k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
+         int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* kept_b,
+         uint32_t* kept_g, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode) {
+  __shared__ uint32_t wbits[KM_WIN / 32];
+  __shared__ uint32_t wcnt[KM_WIN / 2];
+  const uint32_t G = (B0 > 0 && mapmode <= 1) ? label[uf_find_ro(uf, B0 - 1)] : INV;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint64_t edges = 0, kept = 0, inb = 0;
-  for (uint64_t base = e_begin + wave * 64; base < e_end; base += nwaves * 64) {
-    uint64_t idx = base + lane;
-    bool valid = idx < e_end;
-    uint64_t it = valid ? items[idx] : ~0ull;
-    uint32_t b = (uint32_t)(it >> 32);
-    uint32_t a = valid ? (uint32_t)it : 0u;
-    uint32_t g = a;
-    if (valid && a < B0 && mapmode != 2) g = label[uf_find<false>(uf, a)];
-    // keep the first lane of every distinct (g, b) in the wave
-    bool keep = valid;
-    uint64_t rem = mapmode == 1 ? 0ull : __ballot(valid);
-    while (rem) {
-      int leader = __ffsll((unsigned long long)rem) - 1;
-      uint32_t lb = __builtin_amdgcn_readlane(b, leader);
-      uint32_t lg = __builtin_amdgcn_readlane(g, leader);
-      uint64_t same = __ballot(valid && b == lb && g == lg);
-      if (lane != leader && ((same >> lane) & 1)) keep = false;
-      rem &= ~same;
+  for (uint64_t c0 = e_begin + (uint64_t)blockIdx.x * KM_CHUNK; c0 < e_end;
+       c0 += (uint64_t)gridDim.x * KM_CHUNK) {
+    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, e_end);
+    // every record of the chunk has b >= the first record's group start
+    const uint32_t bbase = (((uint32_t)(items[c0] >> 32) >> gshift) << gshift) & ~31u;
+    const uint32_t blast = (uint32_t)(items[c1 - 1] >> 32);
+    const uint32_t gend = (uint32_t)min((((uint64_t)(blast >> gshift)) + 1) << gshift,
+                                        (uint64_t)bbase + KM_WIN);
+    const uint32_t span = gend - bbase;  // ranks of the window that can hold records
+    for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) wbits[i] = 0;
+    if (cnt)
+      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) wcnt[i] = 0;
+    __syncthreads();
+    for (uint64_t base = c0 + (uint64_t)w * 64; base < c1; base += (KM_THREADS / 64) * 64) {
+      uint64_t idx = base + lane;
+      bool valid = idx < c1;
+      uint64_t it = valid ? items[idx] : ~0ull;
+      uint32_t b = (uint32_t)(it >> 32);
+      uint32_t a = valid ? (uint32_t)it : 0u;
+      uint32_t g = a;
+      if (valid && a < B0 && mapmode != 2) g = label[uf_find<false>(uf, a)];
+      // dedupe (mapmode 1): keep the first lane of every distinct (g, b) in the wave.  Off by
+      // default: records are in stream order inside a group, so a wave holds ~60 distinct
+      // pairs (the loop costs more than the zipper saves); the giant's pairs, which are most
+      // of the duplicates, become bitmap marks anyway.
+      bool keep = valid;
+      uint64_t rem = mapmode == 1 ? __ballot(valid) : 0ull;
+      while (rem) {
+        int leader = __ffsll((unsigned long long)rem) - 1;
+        uint32_t lb = __builtin_amdgcn_readlane(b, leader);
+        uint32_t lg = __builtin_amdgcn_readlane(g, leader);
+        uint64_t same = __ballot(valid && b == lb && g == lg);
+        if (lane != leader && ((same >> lane) & 1)) keep = false;
+        rem &= ~same;
+      }
+      if (STATS) { edges += valid; kept += keep; inb += keep && a >= B0; }
+      const uint32_t o = b - bbase;
+      if (valid && cnt) {
+        if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
+        else atomicAdd(&cnt[b], 1u);
+      }
+      bool giant = keep && g == G;
+      if (giant) {
+        if (o < span) atomicOr(&wbits[o >> 5], 1u << (o & 31));
+        else atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+      }
+      // kept pairs stay in place (INVALID holes): no shared append cursor
+      if (valid) {
+        kept_b[idx - e_begin] = (keep && !giant) ? b : INV;
+        kept_g[idx - e_begin] = g;
+      }
     }
-    if (STATS) { edges += valid; kept += keep; inb += keep && a >= B0; }
-    bool giant = keep && g == G;
-    // A hub's (G, b) edges span many waves; only the first wave of the run marks b (a wave
-    // whose b continues from the previous item skips when that item maps to G too: its wave
-    // marked, or skipped by the same rule).  Same-word atomics from every wave serialise.
-    uint32_t pb = INV, pg = INV;
-    if (G != INV && base > e_begin && lane == 0) {
-      uint64_t pit = items[base - 1];
-      uint32_t pa = (uint32_t)pit;
-      pb = (uint32_t)(pit >> 32);
-      pg = pa < B0 ? label[uf_find_ro(uf, pa)] : pa;
-    }
-    pb = __builtin_amdgcn_readfirstlane(pb);
-    pg = __builtin_amdgcn_readfirstlane(pg);
-    if (giant && !(b == pb && pg == G)) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
-    // kept pairs stay in place (INVALID holes): no shared append cursor
-    if (valid) {
-      kept_b[idx - e_begin] = (keep && !giant) ? b : INV;
-      kept_g[idx - e_begin] = g;
-    }
+    __syncthreads();
+    for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS)
+      if (wbits[i]) atomicOr(&bitmap[(bbase >> 5) + i], wbits[i]);
+    if (cnt)
+      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {
+        uint32_t v = wcnt[i];
+        if (v & 0xFFFFu) atomicAdd(&cnt[bbase + 2 * i], v & 0xFFFFu);
+        if (v >> 16) atomicAdd(&cnt[bbase + 2 * i + 1], v >> 16);
+      }
+    __syncthreads();
   }
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
@@ -1225,7 +1358,7 @@ __device__ __forceinline__ uint64_t lower_bound_hi(const uint64_t* a, uint64_t n
 // no union-find help: its in-bucket walks are long).  out[2i] = rank B, out[2i+1] = first
 // edge with hi >= B; entry K_e + K_r carries (INVALID, m_valid).  The host merges and sorts.
 __global__ void k_kb_bounds(const uint64_t* __restrict__ items, uint64_t n, uint32_t K_e,
-                            uint32_t K_r, uint32_t n_seq, unsigned long long* out) {
+                            uint32_t K_r, uint32_t n_seq, int gshift, unsigned long long* out) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t K = K_e + K_r;
   if (k > K) return;
@@ -1238,14 +1371,15 @@ __global__ void k_kb_bounds(const uint64_t* __restrict__ items, uint64_t n, uint
   } else {
     B = (uint32_t)((uint64_t)n_seq * (k - K_e) / K_r);
   }
+  B = (B >> gshift) << gshift;  // items are sorted by hi down to groups of 2^gshift ranks
   out[2 * k] = B;
   out[2 * k + 1] = lower_bound_hi(items, mv, B);
 }
 
 void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
-                      uint32_t n_seq, unsigned long long* out, hipStream_t s) {
+                      uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s) {
   hipLaunchKernelGGL(k_kb_bounds, dim3((K_e + K_r + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s,
-                     items, n, K_e, K_r, n_seq, out);
+                     items, n, K_e, K_r, n_seq, gshift, out);
 }
 
 // counters: 4 device words, zero before the first bucket ([1] n_linked, [2] n_spine; each
@@ -1253,21 +1387,21 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
                       uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, bool stats,
-                      unsigned long long* st, hipStream_t s) {
+                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, int gshift,
+                      uint32_t* cnt, bool stats, unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
-  int mapmode = em ? atoi(em) : 0;  // 0: giant spine on; 3: off (ablation)
+  int mapmode = em ? atoi(em) : 0;  // 0: giant spine on; 1: + wave dedupe; 2: no UF map; 3: spine off
   const char* esl = getenv("SHEEP_KB_SCAN");
   uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
-  bool giant = mapmode == 0 && B0 > 0;
+  bool giant = mapmode <= 1 && B0 > 0;
   if (e_end > e_begin) {
-    uint64_t waves = (e_end - e_begin + 63) / 64;
-    unsigned grid = grid_for(waves * 64);
+    uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
+    unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
     auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-    hipLaunchKernelGGL(mk, dim3(grid), dim3(BLOCK), 0, s, items, e_begin, e_end, B0, uf,
-                       (const uint32_t*)label, kept_b, kept_g, bitmap, st, mapmode);
+    hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
+                       uf, (const uint32_t*)label, kept_b, kept_g, bitmap, cnt, st, mapmode);
     if (giant)
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);

@@ -226,6 +226,8 @@ def test_sharded_partial_trees_with_degree_pst(oracle, gpu, seed):
 
 KB_KNOBS = [
     {},                                                    # defaults (giant spine on)
+    {"SHEEP_KB_MAPMODE": "1"},                             # spine + wave dedupe
+    {"SHEEP_KB_MAPMODE": "2"},                             # no union-find map (walk from a)
     {"SHEEP_KB_MAPMODE": "3"},                             # spine off
     {"SHEEP_KB_SCAN": "1"},                                # runs cut at every gap > 1 word
     {"SHEEP_KB_SCAN": "0", "SHEEP_KB_BUCKETS": "256"},     # every word its own run
