@@ -117,3 +117,33 @@ extern "C" int edge_lab(int variant, const void* uv, uint64_t m, const void* ran
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// One-endpoint gather (rank[rec.y]) over records, one tile of 8192 records per block.
+// xcd: 0 = tile = blockIdx; 1 = XCD-contiguous tiles (blockIdx % 8 picks the XCD's range).
+__global__ void __launch_bounds__(1024) k_gather1(const uint2* __restrict__ uv, uint64_t m,
+                                                  const uint32_t* __restrict__ rank,
+                                                  uint64_t* __restrict__ out, int xcd, uint32_t ntiles) {
+  uint32_t tile = blockIdx.x;
+  if (xcd) {
+    uint32_t per = (ntiles + 7) / 8;
+    tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (tile >= ntiles) return;
+  }
+  uint64_t base = (uint64_t)tile * 8192 + threadIdx.x;
+  uint2 e[8];
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { uint64_t i = base + k * 1024; e[k] = i < m ? uv[i] : make_uint2(0, 0); }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = rank[e[k].y];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { uint64_t i = base + k * 1024; if (i < m) out[i] = ((uint64_t)e[k].x << 32) | r[k]; }
+}
+
+extern "C" int gather_lab(int xcd, const void* uv, uint64_t m, const void* rank, void* out, void* stream) {
+  uint32_t nt = (uint32_t)((m + 8191) / 8192);
+  uint32_t grid = xcd ? ((nt + 7) / 8) * 8 : nt;
+  hipLaunchKernelGGL(k_gather1, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint2*)uv, m,
+                     (const uint32_t*)rank, (uint64_t*)out, xcd, nt);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

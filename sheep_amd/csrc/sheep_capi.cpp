@@ -211,8 +211,18 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   // pst from degrees (di) needs the run length of every hi: counted by k_kb_map.  Otherwise
   // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
   bool pst_count = kb && di;
-  launch_edge_pass_tiles(d_uv, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
-                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s);
+  // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
+  const char* ep = getenv("SHEEP_EDGE_PART");
+  bool part = ep ? atoi(ep) != 0 : m >= (1ull << 22);
+  const uint32_t* src = d_uv;
+  if (part) {
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s);
+    src = (const uint32_t*)items_b;
+    if (tm) tm->mark("partition");
+  }
+  launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
+                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
   if (tm) tm->mark("edge_pass");
   const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
   uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer

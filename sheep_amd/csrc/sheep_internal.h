@@ -69,7 +69,11 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 // edge pass + the first radix pass's tile histograms (sort bits from `shift`, DB wide)
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                             uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
-                            uint32_t* tmp, hipStream_t s);
+                            uint32_t* tmp, hipStream_t s, bool pre = false);
+// Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
+// m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
+void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
                            hipStream_t s);

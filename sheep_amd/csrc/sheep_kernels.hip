@@ -717,10 +717,14 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 
 // The edge pass fused with the first radix pass's tile histograms (digit = bits
 // [shift, shift + DB) of hi): one block per RS_TILE records, wave-striped like
-// k_rsort_count; each thread loads its 8 records and issues their 16 rank gathers before using
-// any (the pass is bound by the random gathers: keep many in flight).  pst (nullable) as in
-// k_edge_pass.
-template <int DB>
+// k_rsort_count; each thread loads its 8 records and issues their rank gathers before using
+// any (keep many gathers in flight).  pst (nullable) as in k_edge_pass.
+// PRE: the records are k_part's output (x, ry): rank[y] was gathered already (or is one of the
+// sentinels RY_SELF / RY_OUT), only rank[x] is gathered here.
+constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
+constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
+
+template <int DB, bool PRE>
 __global__ void __launch_bounds__(RS_THREADS)
 k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
                   uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
@@ -736,13 +740,17 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     uint64_t idx = base + (uint64_t)k * 64;
-    e[k] = idx < m ? uv[idx] : make_uint2(0, 0);
+    e[k] = idx < m ? uv[idx] : make_uint2(0, PRE ? RY_SELF : 0u);
   }
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
-    bool g = e[k].x != e[k].y;  // self-loops (and padding) gather nothing
-    rx[k] = (g && e[k].x < n_rank) ? rank[e[k].x] : INV;
-    ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
+    if (PRE) {
+      rx[k] = (e[k].y != RY_SELF && e[k].x < n_rank) ? rank[e[k].x] : INV;
+    } else {
+      bool g = e[k].x != e[k].y;  // self-loops (and padding) gather nothing
+      rx[k] = (g && e[k].x < n_rank) ? rank[e[k].x] : INV;
+      ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -750,13 +758,17 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
     uint64_t idx = base + (uint64_t)k * 64;
     bool valid = idx < m;
     uint32_t hi = INV, lo = INV;
-    if (valid && e[k].x != e[k].y) {
-      bool ox = e[k].x >= n_rank, oy = e[k].y >= n_rank;
-      if ((ox && ry[k] != INV) || (oy && rx[k] != INV)) {
+    bool loop = PRE ? e[k].y == RY_SELF : e[k].x == e[k].y;
+    if (valid && !loop) {
+      bool ox = e[k].x >= n_rank, oy;
+      uint32_t r_y;
+      if (PRE) { oy = e[k].y == RY_OUT; r_y = oy ? INV : e[k].y; }
+      else { oy = e[k].y >= n_rank; r_y = ry[k]; }
+      if ((ox && r_y != INV) || (oy && rx[k] != INV)) {
         atomicOr(err, ERR_RANGE);
       } else {
-        lo = min(rx[k], ry[k]);
-        hi = max(rx[k], ry[k]);
+        lo = min(rx[k], r_y);
+        hi = max(rx[k], r_y);
         if (lo != INV && pst) atomicAdd(&pst[lo], 1u);
       }
     }
@@ -772,17 +784,157 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
 
 // Edge pass whose output feeds radix_sort_u64(..., bit_lo = shift, counted0 = true): tmp is
 // that sort's tmp (rsort_tmp_words(m)); DB = rsort_first_width of the sorted bit range.
+// pre: uv holds k_part's (x, ry) records.
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                             uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
-                            uint32_t* tmp, hipStream_t s) {
+                            uint32_t* tmp, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
-  if (DB > 8)
-    hipLaunchKernelGGL(k_edge_pass_tiles<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s,
-                       (const uint2*)uv, m, rank, n_rank, pst, items, err, shift, tmp, (uint32_t)nt);
-  else
-    hipLaunchKernelGGL(k_edge_pass_tiles<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s,
-                       (const uint2*)uv, m, rank, n_rank, pst, items, err, shift, tmp, (uint32_t)nt);
+  auto k = DB > 8 ? (pre ? k_edge_pass_tiles<9, true> : k_edge_pass_tiles<9, false>)
+                  : (pre ? k_edge_pass_tiles<8, true> : k_edge_pass_tiles<8, false>);
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
+                     pst, items, err, shift, tmp, (uint32_t)nt);
+}
+
+// ---------------------------------------------------------------------------------------
+// Partitioned rank gathers.  rank[] (4 B per id, 268 MB at RMAT-26) is far beyond L2 and the
+// stream evicts it from the Infinity Cache: gathered in stream order, every lookup is a 64-B
+// HBM access (~60 G lookups/s, 2 per record).  Partitioned by the looked-up id's top 8 bits,
+// the records of one tile look up one 1 MB slice: 3x faster per lookup (measured), for one
+// partition pass (8 B read + 8 B written per record).  So:
+//   k_part<0>: records (x, y) partitioned by y's digit;                 (x-digit histogram)
+//   k_part<1>: ... gather ry = rank[y] and partition (x, ry) by x's digit;
+//   k_edge_pass_tiles<PRE>: gather rank[x] in x-digit order.
+// Order inside a digit is not kept (tiles reserve their runs with one atomic per digit):
+// nothing downstream depends on record order.  Digit = min(id >> sh, 255).
+// ---------------------------------------------------------------------------------------
+static constexpr int PT_THREADS = 1024;
+static constexpr int PT_ITEMS = 16;
+static constexpr int PT_TILE = PT_THREADS * PT_ITEMS;  // 16384 records, 128 KB LDS stage
+
+__device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, 255u); }
+
+// Global histogram of the y digits (the first partition's run sizes).
+__global__ void __launch_bounds__(PT_THREADS)
+k_part_count(const uint2* __restrict__ uv, uint64_t m, int sh, uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t hist[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS) hist[i] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * PT_THREADS + threadIdx.x; i < m;
+       i += (uint64_t)gridDim.x * PT_THREADS)
+    atomicAdd(&hist[part_digit(uv[i].y, sh)], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS)
+    if (hist[i]) atomicAdd(&ghist[i], hist[i]);
+}
+
+// cursor[d] = exclusive prefix of hist (one block of 256 threads); hist is then cleared.
+__global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
+  __shared__ unsigned long long s[256];
+  uint32_t t = threadIdx.x;
+  s[t] = hist[t];
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int i = 0; i < 256; ++i) { unsigned long long v = s[i]; s[i] = run; run += v; }
+  }
+  __syncthreads();
+  cursor[t] = s[t];
+  hist[t] = 0;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(PT_THREADS)
+k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
+       unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh,
+       const uint32_t* __restrict__ rank, uint32_t n_rank) {
+  __shared__ uint64_t stage[PT_TILE];
+  __shared__ uint32_t hist[256], tstart[256], hx[256], wsum[PT_THREADS / 64];
+  __shared__ unsigned long long gbase[256];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * PT_TILE;
+  const uint32_t tile_n = (uint32_t)min((uint64_t)PT_TILE, m - tbase);
+  if (t < 256) { hist[t] = 0; hx[t] = 0; }
+  uint64_t rec[PT_ITEMS];
+  uint32_t li[PT_ITEMS];
+#pragma unroll
+  for (int k = 0; k < PT_ITEMS; ++k) {
+    uint32_t j = (uint32_t)k * PT_THREADS + t;
+    rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+  }
+  if (MODE == 1) {  // (x, y) -> (x, ry)
+    uint32_t ry[PT_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      uint32_t x = (uint32_t)rec[k], y = (uint32_t)(rec[k] >> 32);
+      ry[k] = (x != y && y < n_rank) ? rank[y] : INV;
+    }
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      uint32_t x = (uint32_t)rec[k], y = (uint32_t)(rec[k] >> 32);
+      uint32_t v = x == y ? RY_SELF : (y >= n_rank ? RY_OUT : ry[k]);
+      rec[k] = ((uint64_t)v << 32) | x;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PT_ITEMS; ++k) {
+    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      li[k] = atomicAdd(&hist[part_digit(key, sh)], 1u);
+      if (MODE == 0) atomicAdd(&hx[part_digit((uint32_t)rec[k], sh)], 1u);
+    }
+  }
+  __syncthreads();
+  if (t < 256) {
+    uint32_t c = hist[t];
+    uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[w] = incl;
+    tstart[t] = incl - c;
+    gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;
+    if (MODE == 0 && hx[t]) atomicAdd(&xhist[t], hx[t]);
+  }
+  __syncthreads();
+  if (t < 256) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    tstart[t] += add;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PT_ITEMS; ++k) {
+    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      stage[tstart[part_digit(key, sh)] + li[k]] = rec[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < tile_n; j += PT_THREADS) {
+    uint64_t r = stage[j];
+    uint32_t d = part_digit(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
+    out[gbase[d] + (j - tstart[d])] = r;
+  }
+}
+
+// uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: 512 u32 + 256 u64.
+void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s) {
+  if (m == 0) return;
+  int bits = 0;
+  for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
+  int sh = bits > 8 ? bits - 8 : 0;
+  uint32_t* yhist = ws;
+  uint32_t* xhist = ws + 256;
+  unsigned long long* cursor = (unsigned long long*)(ws + 512);
+  (void)hipMemsetAsync(ws, 0, 512 * 4, s);
+  hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
+  hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
+  uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
+  hipLaunchKernelGGL(k_part<0>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)uv, m,
+                     mid, cursor, xhist, sh, rank, n_rank);
+  hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, xhist, cursor);
+  hipLaunchKernelGGL(k_part<1>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)mid, m,
+                     pre, cursor, xhist, sh, rank, n_rank);
 }
 
 // ---------------------------------------------------------------------------------------
