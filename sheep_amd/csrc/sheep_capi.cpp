@@ -252,8 +252,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     (void)hipMemsetAsync(counters, 0, 16, s);
     (void)hipMemsetAsync(bitmap, 0, ((size_t)n_seq / 32 + 2) * 4, s);
     // the sort's free ping-pong buffer holds the kept (b, g) pairs of a bucket
-    uint32_t* kept_b = (uint32_t*)spare;
-    uint32_t* kept_g = (uint32_t*)spare + m;
+    uint64_t* kept = spare;
     unsigned long long* bounds =
         (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
     launch_iota(uf, n_seq, s);
@@ -278,8 +277,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     for (size_t k = 0; k + 1 < bk.size(); ++k) {
       if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
       launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
-                       label, d_parent, jump, kept_b, kept_g, linked, bitmap, spq, counters,
-                       lo_bit, hcnt, stats, ws, s);
+                       label, d_parent, jump, kept, linked, bitmap, spq, counters, lo_bit, hcnt,
+                       stats, ws, s);
       if (per_bucket) {
         unsigned long long h[16];
         HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));

@@ -84,8 +84,8 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
                       uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s);
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
-                      uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, int gshift,
+                      uint32_t* jump, uint64_t* kept, uint32_t* linked, uint32_t* bitmap,
+                      uint32_t* spq, uint32_t* counters, int gshift,
                       uint32_t* cnt /* nullable: hi run lengths */, bool stats,
                       unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);

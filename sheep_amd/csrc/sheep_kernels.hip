@@ -1136,20 +1136,17 @@ __global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint
 // followed by the kept (b, g) pairs of a bucket.
 struct EdgeSrc {
   const uint64_t* items;  // packed (hi << 32 | lo)
-  const uint32_t* hi;     // or hi[] / lo[]
-  const uint32_t* lo;
-  // kb bucket mode (items == nullptr): indices [0, np) are giant-path edges (G, spq[i]),
-  // then [np, np + nk) the kept pairs.
+  // kb bucket mode (spq != nullptr): indices [0, np) are giant-path edges (G, spq[i]), then
+  // [np, n) the kept pairs items[i - np].
   const uint32_t* spq = nullptr;
   uint32_t G = INV;
   uint64_t np = 0;
   __device__ __forceinline__ void get(uint64_t i, uint32_t& b, uint32_t& a, uint32_t& fl) const {
     fl = 0;
-    if (items) { uint64_t it = items[i]; b = (uint32_t)(it >> 32); a = (uint32_t)it; return; }
     if (i < np) { b = spq[i]; a = G; fl = ZF_KEEP; return; }
-    i -= np;
-    b = hi[i];
-    a = (b != INV) ? lo[i] : 0u;
+    uint64_t it = items[i - np];
+    b = (uint32_t)(it >> 32);
+    a = (uint32_t)it;
   }
 };
 
@@ -1215,7 +1212,7 @@ template <int LOAD, int JUMP, bool STATS>
 __global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
                              uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
   (void)next;
-  EdgeSrc src{items, nullptr, nullptr};
+  EdgeSrc src{items};
   tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, stats, ZRec());
 }
 
@@ -1324,13 +1321,16 @@ static constexpr uint32_t KM_WIN = 32768;   // ranks
 template <bool STATS>
 __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
-         int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* kept_b,
-         uint32_t* kept_g, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode) {
+         int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
+         uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
+  __shared__ uint32_t woff[KM_THREADS / 64 + 1];
+  constexpr int R = KM_CHUNK / KM_THREADS;  // rounds per wave per chunk
   const uint32_t G = (B0 > 0 && mapmode <= 1) ? label[uf_find_ro(uf, B0 - 1)] : INV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint64_t edges = 0, kept = 0, inb = 0;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t edges = 0, kept_n = 0, inb = 0;
   for (uint64_t c0 = e_begin + (uint64_t)blockIdx.x * KM_CHUNK; c0 < e_end;
        c0 += (uint64_t)gridDim.x * KM_CHUNK) {
     const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, e_end);
@@ -1344,8 +1344,11 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
     if (cnt)
       for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) wcnt[i] = 0;
     __syncthreads();
-    for (uint64_t base = c0 + (uint64_t)w * 64; base < c1; base += (KM_THREADS / 64) * 64) {
-      uint64_t idx = base + lane;
+    uint64_t out[R];  // this lane's kept pair per round (b == INVALID: none)
+    uint32_t nout = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint64_t idx = c0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
       bool valid = idx < c1;
       uint64_t it = valid ? items[idx] : ~0ull;
       uint32_t b = (uint32_t)(it >> 32);
@@ -1366,7 +1369,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
         if (lane != leader && ((same >> lane) & 1)) keep = false;
         rem &= ~same;
       }
-      if (STATS) { edges += valid; kept += keep; inb += keep && a >= B0; }
+      if (STATS) { edges += valid; kept_n += keep; inb += keep && a >= B0; }
       const uint32_t o = b - bbase;
       if (valid && cnt) {
         if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
@@ -1377,12 +1380,11 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
         if (o < span) atomicOr(&wbits[o >> 5], 1u << (o & 31));
         else atomicOr(&bitmap[b >> 5], 1u << (b & 31));
       }
-      // kept pairs stay in place (INVALID holes): no shared append cursor
-      if (valid) {
-        kept_b[idx - e_begin] = (keep && !giant) ? b : INV;
-        kept_g[idx - e_begin] = g;
-      }
+      bool k2 = keep && !giant;
+      out[r] = k2 ? (((uint64_t)b << 32) | g) : ~0ull;
+      nout += (uint32_t)__popcll(__ballot(k2));
     }
+    if (lane == 0) woff[w] = nout;
     __syncthreads();
     for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS)
       if (wbits[i]) atomicOr(&bitmap[(bbase >> 5) + i], wbits[i]);
@@ -1392,11 +1394,25 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
         if (v & 0xFFFFu) atomicAdd(&cnt[bbase + 2 * i], v & 0xFFFFu);
         if (v >> 16) atomicAdd(&cnt[bbase + 2 * i + 1], v >> 16);
       }
+    // compaction: one reservation per chunk for the kept pairs of all its waves
+    if (t == 0) {
+      uint32_t run = 0;
+      for (int i = 0; i < KM_THREADS / 64; ++i) { uint32_t v = woff[i]; woff[i] = run; run += v; }
+      woff[KM_THREADS / 64] = run ? atomicAdd(n_kept, run) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = woff[KM_THREADS / 64] + woff[w];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint64_t bal = __ballot(out[r] != ~0ull);
+      if (out[r] != ~0ull) kept[pos + __popcll(bal & lt)] = out[r];
+      pos += (uint32_t)__popcll(bal);
+    }
     __syncthreads();
   }
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
-    atomicAdd(&stats[5], (unsigned long long)kept);
+    atomicAdd(&stats[5], (unsigned long long)kept_n);
     atomicAdd(&stats[6], (unsigned long long)inb);
   }
 }
@@ -1440,20 +1456,20 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 // The kb in-bucket pass: the spine queue, then the kept (b, g) pairs of the bucket, through
 // the balanced lane queue with the spine rules (SpineInfo), recording pre-bucket roots it links.
 template <bool STATS>
-__global__ void k_kb_zip(const uint32_t* __restrict__ kb, const uint32_t* __restrict__ kg,
-                         uint64_t nk, const uint32_t* __restrict__ bitmap,
-                         const uint32_t* __restrict__ spq, const uint32_t* __restrict__ n_spine,
-                         uint32_t B0, uint32_t B1, uint32_t* uf, const uint32_t* __restrict__ label,
-                         uint32_t* parent, uint32_t* jump, unsigned long long* stats,
-                         uint32_t* linked, uint32_t* n_linked, int giant, uint32_t scan_limit,
-                         uint32_t qchunk) {
+__global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __restrict__ n_kept,
+                         const uint32_t* __restrict__ bitmap, const uint32_t* __restrict__ spq,
+                         const uint32_t* __restrict__ n_spine, uint32_t B0, uint32_t B1,
+                         uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
+                         uint32_t* jump, unsigned long long* stats, uint32_t* linked,
+                         uint32_t* n_linked, int giant, uint32_t scan_limit, uint32_t qchunk) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
-  EdgeSrc src{nullptr, kb, kg};
-  SpineInfo sp;
+  EdgeSrc src{kept};
+  const uint64_t nk = *n_kept;
   if (giant && B0 > 0) {
+    SpineInfo sp;
     sp.bitmap = bitmap;
     sp.B0 = B0;
     sp.B1 = B1;
@@ -1486,12 +1502,12 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
   }
 }
 
-// counters[1] = n_linked and counters[2] = n_spine are reset here for the next bucket.
+// counters[1] = n_linked, [2] = n_spine, [3] = n_kept are reset here for the next bucket.
 __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
                            uint32_t B0, uint32_t B1, uint32_t* counters) {
   for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
     if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { counters[1] = 0; counters[2] = 0; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) { counters[1] = 0; counters[2] = 0; counters[3] = 0; }
 }
 
 // Bucket boundaries by edge count: thread k finds m_valid (first INVALID hi), takes the rank at
@@ -1534,26 +1550,28 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
                      items, n, K_e, K_r, n_seq, gshift, out);
 }
 
-// counters: 4 device words, zero before the first bucket ([1] n_linked, [2] n_spine; each
-// bucket's label kernel resets them).  spq: (n_seq / 32 + 64) words.
+// counters: 4 device words, zero before the first bucket ([1] n_linked, [2] n_spine, [3]
+// n_kept; each bucket's label kernel resets them).  spq: (n_seq / 32 + 64) words; kept:
+// (e_end - e_begin) u64.
 void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
                       uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
-                      uint32_t* jump, uint32_t* kept_b, uint32_t* kept_g, uint32_t* linked,
-                      uint32_t* bitmap, uint32_t* spq, uint32_t* counters, int gshift,
-                      uint32_t* cnt, bool stats, unsigned long long* st, hipStream_t s) {
+                      uint32_t* jump, uint64_t* kept, uint32_t* linked, uint32_t* bitmap,
+                      uint32_t* spq, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
+                      unsigned long long* st, hipStream_t s) {
   const char* em = getenv("SHEEP_KB_MAPMODE");
   int mapmode = em ? atoi(em) : 0;  // 0: giant spine on; 1: + wave dedupe; 2: no UF map; 3: spine off
   const char* esl = getenv("SHEEP_KB_SCAN");
   uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
+  uint32_t* n_kept = counters + 3;
   bool giant = mapmode <= 1 && B0 > 0;
   if (e_end > e_begin) {
     uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
     unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
     auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
     hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
-                       uf, (const uint32_t*)label, kept_b, kept_g, bitmap, cnt, st, mapmode);
+                       uf, (const uint32_t*)label, kept, n_kept, bitmap, cnt, st, mapmode);
     if (giant)
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);
@@ -1562,11 +1580,10 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
     const char* eg = getenv("SHEEP_KB_ZGRID");
     uint32_t qchunk = eq ? (uint32_t)atoi(eq) : 64;
     unsigned zgrid = eg ? (unsigned)atoi(eg) : MAX_GRID;
-    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, (const uint32_t*)kept_b,
-                       (const uint32_t*)kept_g, e_end - e_begin, (const uint32_t*)bitmap,
-                       (const uint32_t*)spq, (const uint32_t*)n_spine, B0, B1, uf,
-                       (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
-                       giant ? 1 : 0, scan_limit, qchunk);
+    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, (const uint64_t*)kept,
+                       (const uint32_t*)n_kept, (const uint32_t*)bitmap, (const uint32_t*)spq,
+                       (const uint32_t*)n_spine, B0, B1, uf, (const uint32_t*)label, parent, jump,
+                       st + 8, linked, n_linked, giant ? 1 : 0, scan_limit, qchunk);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
