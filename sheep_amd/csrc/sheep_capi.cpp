@@ -72,6 +72,8 @@ static Ctx& init_ctx(int device) {
   HIP_CHECK(hipSetDevice(device));
   if (c.device < 0) {
     HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    for (auto& e : c.kb_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&c.d_err, 16));
     HIP_CHECK(hipMemset(c.d_err, 0, 16));
     HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
@@ -246,13 +248,12 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
     uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
-    uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 64);
-    uint32_t* bitmap = (uint32_t*)c.scratch.get("kb_bitmap", ((size_t)n_seq / 32 + 2) * 4);
-    uint32_t* spq = (uint32_t*)c.scratch.get("kb_spq", ((size_t)n_seq / 32 + 64) * 4);
-    (void)hipMemsetAsync(counters, 0, 16, s);
-    (void)hipMemsetAsync(bitmap, 0, ((size_t)n_seq / 32 + 2) * 4, s);
-    // the sort's free ping-pong buffer holds the kept (b, g) pairs of a bucket
-    uint64_t* kept = spare;
+    uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 2 * 64);
+    const size_t bm_words = (size_t)n_seq / 32 + 2, spq_words = (size_t)n_seq / 32 + 64;
+    uint32_t* bitmaps = (uint32_t*)c.scratch.get("kb_bitmap", 2 * bm_words * 4);
+    uint32_t* spqs = (uint32_t*)c.scratch.get("kb_spq", 2 * spq_words * 4);
+    (void)hipMemsetAsync(counters, 0, 2 * 64, s);
+    (void)hipMemsetAsync(bitmaps, 0, 2 * bm_words * 4, s);
     unsigned long long* bounds =
         (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
     launch_iota(uf, n_seq, s);
@@ -273,18 +274,66 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
       if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
     if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
     bk.emplace_back(n_seq, m_valid);
+    const size_t nb = bk.size() - 1;
+    // The sort's free ping-pong buffer (m items) holds the kept (b, g) pairs of a bucket.
+    // Pipelined (default): bucket k+1 is mapped on the side stream while bucket k is applied
+    // on s, with kept pairs, marks and counters double-buffered by bucket parity — each needs
+    // half of the buffer.  The map of bucket k+1 anchors the giant at the last rank of bucket
+    // k-1 (launch_kb_map).
+    uint64_t max_e = 0;
+    for (size_t k = 0; k < nb; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
+    const char* epp = getenv("SHEEP_KB_PIPE");
     bool per_bucket = es && es[0] == '2';
-    for (size_t k = 0; k + 1 < bk.size(); ++k) {
-      if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
-      launch_kb_bucket(sorted, bk[k].second, bk[k + 1].second, bk[k].first, bk[k + 1].first, uf,
-                       label, d_parent, jump, kept, linked, bitmap, spq, counters, lo_bit, hcnt,
-                       stats, ws, s);
-      if (per_bucket) {
-        unsigned long long h[16];
-        HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
-                k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[8], h[9], h[10], h[11], h[12]);
+    const bool pipe = (epp ? atoi(epp) != 0 : true) && !per_bucket && 2 * max_e <= m;
+    const char* erf = getenv("SHEEP_KB_REFRESH");
+    const bool refresh = erf ? atoi(erf) != 0 : true;
+    uint64_t* kept[2] = {spare, pipe ? spare + m / 2 : spare};
+    auto par = [&](size_t k) { return pipe ? (int)(k & 1) : 0; };
+    auto anchor_of = [&](size_t k) -> uint32_t {
+      size_t a = pipe ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
+      return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
+    };
+    auto map_k = [&](size_t k, hipStream_t st) {
+      int p = par(k);
+      launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
+                    kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws, st);
+    };
+    auto apply_k = [&](size_t k, hipStream_t st) {
+      int p = par(k);
+      launch_kb_apply(bk[k + 1].second > bk[k].second, bk[k].first, bk[k + 1].first, anchor_of(k),
+                      uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
+                      spqs + p * spq_words, counters + p * 16, pipe && refresh, stats, ws, st);
+    };
+    if (pipe) {
+      hipStream_t s2 = c.side;
+      hipEvent_t* ev_map = c.kb_ev;
+      hipEvent_t* ev_apply = c.kb_ev + 2;
+      HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
+      HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
+      map_k(0, s2);
+      HIP_CHECK(hipEventRecord(ev_map[0], s2));
+      for (size_t k = 0; k < nb; ++k) {
+        if (k + 1 < nb) {  // map k+1 reuses the buffers of bucket k-1: wait for its apply
+          if (k >= 1) HIP_CHECK(hipStreamWaitEvent(s2, ev_apply[(k + 1) & 1], 0));
+          map_k(k + 1, s2);
+          HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
+        }
+        HIP_CHECK(hipStreamWaitEvent(s, ev_map[k & 1], 0));
+        apply_k(k, s);
+        HIP_CHECK(hipEventRecord(ev_apply[k & 1], s));
+      }
+    } else {
+      for (size_t k = 0; k < nb; ++k) {
+        if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
+        map_k(k, s);
+        apply_k(k, s);
+        if (per_bucket) {
+          unsigned long long h[16];
+          HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
+          HIP_CHECK(hipStreamSynchronize(s));
+          fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
+                  k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[8], h[9], h[10], h[11], h[12]);
+        }
       }
     }
   }

@@ -27,6 +27,8 @@ struct Scratch {
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;     // second stream of the pipelined kb loop
+  hipEvent_t kb_ev[5] = {};       // kb loop: [0,1] map done, [2,3] apply done (by parity), [4] start
   Scratch scratch;
   uint32_t* d_err = nullptr;     // device error word
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
@@ -82,12 +84,19 @@ void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uin
                         int variant, bool stats, unsigned long long* ws, hipStream_t s);
 void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
                       uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s);
-void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
-                      uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
-                      uint32_t* jump, uint64_t* kept, uint32_t* linked, uint32_t* bitmap,
-                      uint32_t* spq, uint32_t* counters, int gshift,
-                      uint32_t* cnt /* nullable: hi run lengths */, bool stats,
-                      unsigned long long* st, hipStream_t s);
+// One kb bucket in two halves (sheep_kernels.hip): the map (records -> kept pairs + giant marks
+// + hi counts) and the apply (spine, zipper, union-find fold, labels).  counters: this
+// bucket parity's 4 words; anchor: see launch_kb_map.
+void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
+                   uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
+                   uint32_t* bitmap, uint32_t* counters, int gshift,
+                   uint32_t* cnt /* nullable: hi run lengths */, bool stats,
+                   unsigned long long* st, hipStream_t s);
+// refresh: re-resolve the kept starts against the current union-find first (pipelined loop).
+void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
+                     uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
+                     uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
+                     bool refresh, bool stats, unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);

@@ -1295,11 +1295,13 @@ __device__ __forceinline__ uint32_t uf_find_ro(const uint32_t* uf, uint32_t x) {
   return x;
 }
 
-__device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v) {
+// Link order: R (the giant's root, see k_kb_union) above everything, then uf_prio — a strict
+// total order, so concurrent links never close a cycle.
+__device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, uint32_t R) {
   for (;;) {
     uint32_t ru = uf_find<true>(uf, u), rv = uf_find<true>(uf, v);
     if (ru == rv) return;
-    if (uf_prio(ru) > uf_prio(rv)) { uint32_t t = ru; ru = rv; rv = t; }
+    if (ru == R || (rv != R && uf_prio(ru) > uf_prio(rv))) { uint32_t t = ru; ru = rv; rv = t; }
     if (atomicCAS(&uf[ru], ru, rv) == ru) return;
   }
 }
@@ -1322,12 +1324,19 @@ template <bool STATS>
 __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
          int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
-         uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode) {
+         uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode,
+         uint32_t anchor) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
   constexpr int R = KM_CHUNK / KM_THREADS;  // rounds per wave per chunk
-  const uint32_t G = (B0 > 0 && mapmode <= 1) ? label[uf_find_ro(uf, B0 - 1)] : INV;
+  // RG: the giant's union-find root, found from the anchor rank (see launch_kb_map); it does
+  // not move while this map runs (k_kb_union links everything else below it).  G: its
+  // elimination-tree root.  Membership is tested on the root, not on the label, which the
+  // apply of the previous bucket may be rewriting meanwhile.
+  const uint32_t RG = (anchor != INV && mapmode <= 1) ? uf_find_ro(uf, anchor) : INV;
+
+  const uint32_t G = RG != INV ? label[RG] : INV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t edges = 0, kept_n = 0, inb = 0;
@@ -1354,7 +1363,10 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
       uint32_t b = (uint32_t)(it >> 32);
       uint32_t a = valid ? (uint32_t)it : 0u;
       uint32_t g = a;
-      if (valid && a < B0 && mapmode != 2) g = label[uf_find<false>(uf, a)];
+      if (valid && a < B0 && mapmode != 2) {
+        const uint32_t rt = uf_find<false>(uf, a);
+        g = rt == RG ? G : label[rt];
+      }
       // dedupe (mapmode 1): keep the first lane of every distinct (g, b) in the wave.  Off by
       // default: records are in stream order inside a group, so a wave holds ~60 distinct
       // pairs (the loop costs more than the zipper saves); the giant's pairs, which are most
@@ -1453,6 +1465,34 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
   }
 }
 
+// Pipelined loop: the map of this bucket ran while the previous one was being applied, so its
+// kept starts g may be stale — still exact, but from an old root the zipper walks up through
+// everything the previous bucket linked.  With the union-find now current: g' = label[find(g)]
+// (one thread per pair, all chains in flight together); a pair that turns out to reach the
+// giant becomes b's mark (tested before the atomic: most hub words are marked already) and is
+// dropped (b = INVALID, skipped by the zipper).  anchor: the map's and the spine's, so that
+// every mark of the bucket is relative to one component.
+__global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept,
+                             uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* bitmap,
+                             uint32_t B0, uint32_t anchor) {
+  const uint32_t nk = *n_kept;
+  const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
+    const uint64_t it = kept[i];
+    const uint32_t g = (uint32_t)it, b = (uint32_t)(it >> 32);
+    if (g >= B0) continue;
+    const uint32_t rt = uf_find<false>(uf, g);
+    if (rt == RG) {
+      const uint32_t bit = 1u << (b & 31);
+      if (!(bitmap[b >> 5] & bit)) atomicOr(&bitmap[b >> 5], bit);
+      kept[i] = ~0ull;
+    } else {
+      const uint32_t g2 = label[rt];
+      if (g2 != g) kept[i] = ((uint64_t)b << 32) | g2;
+    }
+  }
+}
+
 // The kb in-bucket pass: the spine queue, then the kept (b, g) pairs of the bucket, through
 // the balanced lane queue with the spine rules (SpineInfo), recording pre-bucket roots it links.
 template <bool STATS>
@@ -1461,19 +1501,20 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
                          const uint32_t* __restrict__ n_spine, uint32_t B0, uint32_t B1,
                          uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
                          uint32_t* jump, unsigned long long* stats, uint32_t* linked,
-                         uint32_t* n_linked, int giant, uint32_t scan_limit, uint32_t qchunk) {
+                         uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
+                         uint32_t qchunk) {
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
   EdgeSrc src{kept};
   const uint64_t nk = *n_kept;
-  if (giant && B0 > 0) {
+  if (anchor != INV) {
     SpineInfo sp;
     sp.bitmap = bitmap;
     sp.B0 = B0;
     sp.B1 = B1;
-    sp.G = label[uf_find_ro(uf, B0 - 1)];
+    sp.G = label[uf_find_ro(uf, anchor)];
     sp.limit = scan_limit;
     src.spq = spq;
     src.G = sp.G;
@@ -1484,9 +1525,15 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   }
 }
 
+// anchor: rank B0 - 1 (INV for the first bucket).  Its root R is never linked below another
+// root here, so the giant keeps one root from bucket to bucket: the map of the next bucket,
+// which runs concurrently in the pipelined loop, finds the same R from the same rank.  (All
+// threads read the same R: no union of this launch can move it.)
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
                            uint32_t B1, const uint32_t* __restrict__ linked,
-                           const uint32_t* __restrict__ n_linked, uint32_t* bitmap) {
+                           const uint32_t* __restrict__ n_linked, uint32_t* bitmap,
+                           uint32_t anchor) {
+  const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
   // with the next bucket hold no marks of it yet; the previous bucket cleared its own)
   for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
@@ -1498,7 +1545,7 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t v = i < width ? B0 + (uint32_t)i : linked[i - width];
     uint32_t p = parent[v];
-    if (p != INV) uf_union(uf, v, p);
+    if (p != INV) uf_union(uf, v, p, R);
   }
 }
 
@@ -1550,29 +1597,52 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
                      items, n, K_e, K_r, n_seq, gshift, out);
 }
 
-// counters: 4 device words, zero before the first bucket ([1] n_linked, [2] n_spine, [3]
-// n_kept; each bucket's label kernel resets them).  spq: (n_seq / 32 + 64) words; kept:
-// (e_end - e_begin) u64.
-void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
-                      uint32_t B0, uint32_t B1, uint32_t* uf, uint32_t* label, uint32_t* parent,
-                      uint32_t* jump, uint64_t* kept, uint32_t* linked, uint32_t* bitmap,
-                      uint32_t* spq, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
-                      unsigned long long* st, hipStream_t s) {
+// counters: 4 device words per bucket parity, zero before the first bucket ([1] n_linked,
+// [2] n_spine, [3] n_kept; each bucket's label kernel resets its set).  spq: (n_seq / 32 + 64)
+// words; kept: (e_end - e_begin) u64.
+//
+// The anchor is a rank whose component is taken as the giant: its elimination-tree root G is
+// found when the map starts (marks) and again when the zipper starts (spine).  Any rank whose
+// bucket has been applied before the map starts is exact: the two finds may see different
+// roots while earlier buckets are still being folded into the union-find, but both lie in the
+// anchor's component at rank B0, and an edge (a, b >= B0) may be moved to any vertex of a's
+// component at B0.  (The pipelined loop maps bucket k+1 while bucket k is applied, so it
+// anchors at the last rank of bucket k-1.)  INV: no giant (first buckets, mapmode >= 2).
+static int kb_mapmode() {
   const char* em = getenv("SHEEP_KB_MAPMODE");
-  int mapmode = em ? atoi(em) : 0;  // 0: giant spine on; 1: + wave dedupe; 2: no UF map; 3: spine off
+  return em ? atoi(em) : 0;  // 0: giant spine on; 1: + wave dedupe; 2: no UF map; 3: spine off
+}
+
+void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
+                   uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
+                   uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
+                   unsigned long long* st, hipStream_t s) {
+  const int mapmode = kb_mapmode();
+  if (mapmode > 1) anchor = INV;
+  if (e_end <= e_begin) return;
+  uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
+  unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
+  auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
+  hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
+                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor);
+}
+
+void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
+                     uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
+                     uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
+                     bool refresh, bool stats, unsigned long long* st, hipStream_t s) {
+  const int mapmode = kb_mapmode();
+  if (mapmode > 1) anchor = INV;
   const char* esl = getenv("SHEEP_KB_SCAN");
   uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
   uint32_t* n_kept = counters + 3;
-  bool giant = mapmode <= 1 && B0 > 0;
-  if (e_end > e_begin) {
-    uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
-    unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
-    auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-    hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
-                       uf, (const uint32_t*)label, kept, n_kept, bitmap, cnt, st, mapmode);
-    if (giant)
+  if (nonempty) {
+    if (refresh)
+      hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
+                         uf, (const uint32_t*)label, bitmap, B0, anchor);
+    if (anchor != INV)
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
@@ -1580,14 +1650,15 @@ void launch_kb_bucket(const uint64_t* items, uint64_t e_begin, uint64_t e_end,
     const char* eg = getenv("SHEEP_KB_ZGRID");
     uint32_t qchunk = eq ? (uint32_t)atoi(eq) : 64;
     unsigned zgrid = eg ? (unsigned)atoi(eg) : MAX_GRID;
-    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, (const uint64_t*)kept,
-                       (const uint32_t*)n_kept, (const uint32_t*)bitmap, (const uint32_t*)spq,
-                       (const uint32_t*)n_spine, B0, B1, uf, (const uint32_t*)label, parent, jump,
-                       st + 8, linked, n_linked, giant ? 1 : 0, scan_limit, qchunk);
+    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
+                       (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
+                       B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
+                       anchor, scan_limit, qchunk);
   }
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
-                     (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap);
+                     (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,
+                     B0 > 0 ? B0 - 1 : INV);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, counters);
 }

@@ -234,6 +234,9 @@ KB_KNOBS = [
     {"SHEEP_KB_BUCKETS": "4", "SHEEP_KB_RANKB": "8"},      # few, wide buckets
     {"SHEEP_KB_BUCKETS": "512", "SHEEP_KB_QCHUNK": "1"},   # many buckets, tiny queue chunks
     {"SHEEP_TREE_ALGO": "zip"},                            # plain zipper, no buckets
+    {"SHEEP_KB_PIPE": "0"},                                # one stream, map of bucket k after apply of k-1
+    {"SHEEP_KB_REFRESH": "0"},                             # pipelined, stale kept starts zipped as they are
+    {"SHEEP_KB_PIPE": "1", "SHEEP_KB_BUCKETS": "512", "SHEEP_KB_RANKB": "512"},  # many narrow buckets
 ]
 
 
