@@ -115,6 +115,14 @@ int sheep_build_tree_deg_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d
 int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_t* d_parent_b,
                           const uint32_t* d_pst_b, uint32_t n, void* stream);
 
+/* d_parent_out <- etree of the union of n_trees forests over the same n ranks, given as
+ * n_trees consecutive parent arrays in d_parents (n_trees * n words; INVALID = root).  The
+ * parent half of an n_trees-way merge (jnode.cpp:174-201 applied pairwise, mpi_merge
+ * jnode.cpp:213-250) done in one build: the edges (v, parent_t[v]) of every tree sorted by
+ * parent and inserted as in graph2tree; pst_weight of a merge is the plain sum.  Synchronises. */
+int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_t n,
+                            uint32_t* d_parent_out, void* stream);
+
 /* The whole single-device hot path: degree -> sequence -> tree (graph2tree's Sorted+Mapped).
  * d_seq holds n_ids entries, d_parent/d_pst hold n_ids entries (n_seq used).  Synchronises. */
 int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,

@@ -4,7 +4,7 @@
 Each rank's work runs back to back on cuda:0 and is timed on its own, so the critical path
 of a real P-GPU run can be estimated: max over ranks of (degree), the degree all-reduce
 (not simulated: a sum on one GPU), the sequence, max over ranks of (partial tree), then
-log2(P) merge rounds (each round's merges are concurrent on different GPUs: max over pairs).
+the P-way forest merge on rank 0 (gather and pst reduce not simulated).
 The merged tree is checked against the single-GPU tree.
 
     python scripts/shard_sim.py [--scale 26] [--ranks 8]
@@ -63,28 +63,24 @@ def main():
             phases = {k: round(v, 3) for k, v in capi.last_timings()}
             trees.append(tr)
             t_build.append(t)
-        rounds = []
-        step = 1
-        while step < P:
-            ts = []
-            for r in range(0, P, 2 * step):
-                if r + step < P:
-                    pa, sa = trees[r]
-                    pb, sb = trees[r + step]
-                    _, t = timed(lambda: device.merge_into(pa, sa, pb, sb, n_seq))
-                    ts.append(t)
-            rounds.append(max(ts))
-            step *= 2
+        pst = trees[0][1].view(torch.int32).clone()
+        for _, s_ in trees[1:]:
+            pst += s_.view(torch.int32)
+        stack = torch.stack([p[:n_seq] for p, _ in trees])
+        merged, t_merge = timed(lambda: device.merge_forests(stack, n_seq))
+        merge_phases = {k: round(v, 3) for k, v in capi.last_timings()}
+        rounds = [t_merge]
         nonroot = [int((p[:n_seq].view(torch.int32) != -1).sum()) for p, _ in trees[:1]]
         res = {"P": P, "scale": a.scale, "n_seq": n_seq,
                "degree_ms": [round(x, 3) for x in t_deg], "sequence_ms": round(t_seq, 3),
                "build_ms": [round(x, 3) for x in t_build], "merge_round_ms": [round(x, 3) for x in rounds],
                "critical_ms_no_comm": round(max(t_deg) + t_seq + max(t_build) + sum(rounds), 3),
-               "rank0_tree_edges": nonroot[0], "last_build_phases": phases}
+               "rank0_tree_edges": nonroot[0], "last_build_phases": phases,
+               "merge_phases": merge_phases}
     # check against the single-GPU tree
     uv = device.rmat(a.scale, 16, a.seed)
     s1, p1, w1, n1 = device.graph2tree(uv, n_ids)
-    p0, w0 = trees[0]
+    p0, w0 = merged, pst.view(torch.uint32)
     res["bit_exact_vs_single"] = bool(n1 == n_seq and torch.equal(p1[:n1].view(torch.int32), p0[:n1].view(torch.int32))
                                       and torch.equal(w1[:n1].view(torch.int32), w0[:n1].view(torch.int32)))
     (_, t1) = timed(lambda: device.graph2tree(uv, n_ids))

@@ -187,54 +187,14 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   return n_seq;
 }
 
-static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
-                           uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
-                           hipStream_t s, Timer* tm, const DegInfo* di = nullptr) {
-  if (n_seq == 0) return;
-  launch_fill(d_parent, INV, n_seq, s);
-  launch_fill(d_pst, 0, n_seq, s);
-  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n_seq * 4);
-  launch_fill(jump, 0, n_seq, s);
-  if (m == 0) return;
-  uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
-  uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
-  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
-  if (tm) tm->mark("tree_init");
-  const char* ea = getenv("SHEEP_TREE_ALGO");
-  bool kb = !(ea && strcmp(ea, "zip") == 0);
+// Liu's elimination tree from items sorted by hi down to groups of 2^lo_bit ranks (m items,
+// INVALID his last): the kb bucket loop (or the plain zipper).  parent: n_seq words, INVALID
+// filled; jump: n_seq zeroed words; spare: m free u64 (kept pairs); hcnt: nullable hi counts.
+static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, uint64_t m,
+                             uint32_t n_seq, int lo_bit, uint32_t* d_parent, uint32_t* jump,
+                             uint32_t* hcnt, bool kb, bool stats, unsigned long long* ws,
+                             hipStream_t s, Timer* tm) {
   const char* es = getenv("SHEEP_TREE_STATS");
-  bool stats = es && (es[0] == '1' || es[0] == '2');
-  // Sort keys: hi's bits [lo_bit, top + 1) — bit `top` puts INVALID his after every rank.
-  // kb needs hi order only down to groups of 2^lo_bit ranks (bucket ranges; wave dedupe and
-  // the run lengths that pst needs are done per group inside k_kb_map): 18 bits = 2 passes.
-  // The plain zipper only needs the top 16 bits (order affects work, never the result).
-  int top = bits_for(n_seq);
-  int lo_bit = std::max(0, top + 1 - (kb ? 18 : 16));
-  // pst from degrees (di) needs the run length of every hi: counted by k_kb_map.  Otherwise
-  // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
-  bool pst_count = kb && di;
-  // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
-  const char* ep = getenv("SHEEP_EDGE_PART");
-  bool part = ep ? atoi(ep) != 0 : m >= (1ull << 22);
-  const uint32_t* src = d_uv;
-  if (part) {
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
-    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s);
-    src = (const uint32_t*)items_b;
-    if (tm) tm->mark("partition");
-  }
-  launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
-                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
-  if (tm) tm->mark("edge_pass");
-  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
-  uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
-  if (tm) tm->mark("bucket_sort");
-  uint32_t* hcnt = nullptr;
-  if (pst_count) {
-    hcnt = (uint32_t*)c.scratch.get("hi_count", (size_t)n_seq * 4);
-    launch_fill(hcnt, 0, n_seq, s);
-  }
-  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   if (!kb) {
     const char* ev = getenv("SHEEP_TREE_VARIANT");
     int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
@@ -337,6 +297,57 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
       }
     }
   }
+}
+
+static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
+                           uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
+                           hipStream_t s, Timer* tm, const DegInfo* di = nullptr) {
+  if (n_seq == 0) return;
+  launch_fill(d_parent, INV, n_seq, s);
+  launch_fill(d_pst, 0, n_seq, s);
+  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n_seq * 4);
+  launch_fill(jump, 0, n_seq, s);
+  if (m == 0) return;
+  uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
+  uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
+  if (tm) tm->mark("tree_init");
+  const char* ea = getenv("SHEEP_TREE_ALGO");
+  bool kb = !(ea && strcmp(ea, "zip") == 0);
+  const char* es = getenv("SHEEP_TREE_STATS");
+  bool stats = es && (es[0] == '1' || es[0] == '2');
+  // Sort keys: hi's bits [lo_bit, top + 1) — bit `top` puts INVALID his after every rank.
+  // kb needs hi order only down to groups of 2^lo_bit ranks (bucket ranges; wave dedupe and
+  // the run lengths that pst needs are done per group inside k_kb_map): 18 bits = 2 passes.
+  // The plain zipper only needs the top 16 bits (order affects work, never the result).
+  int top = bits_for(n_seq);
+  int lo_bit = std::max(0, top + 1 - (kb ? 18 : 16));
+  // pst from degrees (di) needs the run length of every hi: counted by k_kb_map.  Otherwise
+  // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
+  bool pst_count = kb && di;
+  // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
+  const char* ep = getenv("SHEEP_EDGE_PART");
+  bool part = ep ? atoi(ep) != 0 : m >= (1ull << 22);
+  const uint32_t* src = d_uv;
+  if (part) {
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s);
+    src = (const uint32_t*)items_b;
+    if (tm) tm->mark("partition");
+  }
+  launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
+                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
+  if (tm) tm->mark("edge_pass");
+  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
+  uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
+  if (tm) tm->mark("bucket_sort");
+  uint32_t* hcnt = nullptr;
+  if (pst_count) {
+    hcnt = (uint32_t*)c.scratch.get("hi_count", (size_t)n_seq * 4);
+    launch_fill(hcnt, 0, n_seq, s);
+  }
+  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
+  tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, kb, stats, ws, s, tm);
   if (tm) tm->mark("tree_insert");
   if (pst_count) {
     launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s);
@@ -353,6 +364,31 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
       fprintf(stderr, "tree_stats algo=zip edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
               h[1], h[2], h[3], h[4], h[5]);
   }
+}
+
+// etree of the union of T forests over the same n ranks (the multi-GPU reduce): their edges
+// (v, parent_t[v]) as items, sorted by parent, through the kb loop.
+static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uint32_t n,
+                              uint32_t* d_parent, hipStream_t s, Timer* tm) {
+  if (n == 0) return;
+  launch_fill(d_parent, INV, n, s);
+  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n * 4);
+  launch_fill(jump, 0, n, s);
+  const uint64_t m = (uint64_t)T * n;
+  if (m == 0) return;
+  uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
+  uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
+  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
+  for (uint32_t t = 0; t < T; ++t) launch_forest_items(d_parents + (size_t)t * n, n, items + (size_t)t * n, s);
+  if (tm) tm->mark("forest_items");
+  const int top = bits_for(n);
+  const int lo_bit = std::max(0, top + 1 - 18);
+  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, false);
+  uint64_t* spare = (sorted == items) ? items_b : items;
+  if (tm) tm->mark("bucket_sort");
+  unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
+  tree_from_sorted(c, sorted, spare, m, n, lo_bit, d_parent, jump, nullptr, true, false, ws, s, tm);
+  if (tm) tm->mark("tree_insert");
 }
 
 }  // namespace sheep
@@ -454,6 +490,18 @@ int sheep_build_tree_deg_dev(const uint32_t* d_uv, uint64_t m, const uint32_t* d
   di.selfc = d_selfc;
   di.mode = degree_mode;
   build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, &tm, &di);
+  check_err(c, s);
+  tm.finish(c);
+  API_END
+}
+
+int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_t n,
+                            uint32_t* d_parent_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = pick(c, stream);
+  Timer tm(s);
+  merge_forests_dev(c, d_parents, n_trees, n, d_parent_out, s, &tm);
   check_err(c, s);
   tm.finish(c);
   API_END

@@ -98,6 +98,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
                      bool refresh, bool stats, unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
+void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

@@ -1663,6 +1663,18 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      (const uint32_t*)parent, uf, label, B0, B1, counters);
 }
 
+// Items of one forest over n ranks for a union build: (parent[v] << 32 | v); a root's INVALID
+// parent becomes an INVALID hi, which sorts after every rank.
+__global__ void k_forest_items(const uint32_t* __restrict__ parent, uint32_t n,
+                               uint64_t* __restrict__ items) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x)
+    items[v] = ((uint64_t)parent[v] << 32) | v;
+}
+
+void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_forest_items, dim3(grid_for(n)), dim3(BLOCK), 0, s, parent, n, items);
+}
+
 __global__ void k_iota(uint32_t* p, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = i;
 }

@@ -82,6 +82,16 @@ def merge_into(parent_a, pst_a, parent_b, pst_b, n):
               _stream())
 
 
+def merge_forests(parents, n, out=None):
+    """etree of the union of the forests in ``parents`` ((T, >= n) uint32, INVALID = root)."""
+    T = parents.shape[0]
+    parents = parents[:, :n].contiguous()
+    out = out if out is not None else torch.empty(max(n, 1), dtype=torch.uint32,
+                                                  device=parents.device)
+    capi.call("sheep_merge_forests_dev", _p(parents), T, n, _p(out), _stream())
+    return out
+
+
 def graph2tree(uv, n_ids, mode=capi.DEGREE_LLAMA, seq=None, parent=None, pst=None):
     dev = uv.device
     seq = seq if seq is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev)

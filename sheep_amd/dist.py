@@ -5,10 +5,14 @@ This is the MI355X replacement of graph2tree -i -r (graph2tree.cpp:134-200):
   2. per-rank degrees are summed with ONE all-reduce over xGMI (mpiSequence's MPI_Allreduce,
      sequence.h:78) and every rank derives the identical seq/rank map on its own GPU;
   3. every rank builds its partial elimination tree (jtree.cpp:112-145 on its shard);
-  4. partial trees are combined by a log2(P) pairwise reduce to rank 0 (mpi_merge's
-     MPI_Reduce with the merge op, jnode.cpp:213-250; scripts/reduce-worker.sh's pairing):
-     at step s, rank r with r % 2s == s sends (parent, pst) to r - s, which merges in place.
-The merge is exact and associative, so the result equals the serial tree for any P.
+  4. the partial trees are reduced to rank 0 (mpi_merge's MPI_Reduce with the merge op,
+     jnode.cpp:213-250): pst_weight with ONE sum-reduce (the merge adds them, jnode.cpp:
+     174-201), the parent arrays with one gather, after which rank 0 builds the elimination
+     tree of the union of all P forests in a single pass (sheep_merge_forests_dev).  Pairwise
+     merging (the reference's reduce tree, and scripts/reduce-worker.sh) would put log2(P)
+     dependent merges on the critical path; the merge is exact and associative, so one
+     P-way merge gives the same tree.
+The result equals the serial tree for any P.
 
 The kernel operations are injected (``ops``) so the same orchestration runs on the GPU
 (``sheep_amd.device``) and, in the CPU gloo tests, on a test-only backend.
@@ -37,22 +41,22 @@ def build_tree_sharded(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     seq, rmap, n_seq = ops.sequence(deg)
     # pst of the partial tree comes from this shard's own degrees (pre-all-reduce)
     parent, pst = ops.build_tree(uv_shard, rmap, seq, n_seq, deg_local, selfc, mode)
-    step = 1
-    while step < world:
-        if rank % (2 * step) == 0:
-            src = rank + step
-            if src < world:
-                pb = torch.empty_like(parent)
-                sb = torch.empty_like(pst)
-                dist.recv(_i32(pb), src=src, group=group)
-                dist.recv(_i32(sb), src=src, group=group)
-                ops.merge_into(parent, pst, pb, sb, n_seq)
-        elif rank % (2 * step) == step:
-            dist.send(_i32(parent), dst=rank - step, group=group)
-            dist.send(_i32(pst), dst=rank - step, group=group)
-            return seq, None, None, n_seq
-        step *= 2
-    return seq, parent, pst, n_seq
+    if world == 1:
+        return seq, parent, pst, n_seq
+    if timings is not None:
+        timings["partial_tree"] = ops.now()
+    dist.reduce(_i32(pst), dst=0, op=dist.ReduceOp.SUM, group=group)
+    mine = parent[:n_seq].contiguous()
+    if rank == 0:
+        stack = torch.empty((world, n_seq), dtype=parent.dtype, device=parent.device)
+        dist.gather(_i32(mine), gather_list=[_i32(stack[r]) for r in range(world)], dst=0,
+                    group=group)
+        if timings is not None:
+            timings["gather"] = ops.now()
+        parent = ops.merge_forests(stack, n_seq)
+        return seq, parent, pst, n_seq
+    dist.gather(_i32(mine), dst=0, group=group)
+    return seq, None, None, n_seq
 
 
 class DeviceOps:
@@ -74,3 +78,12 @@ class DeviceOps:
 
     def merge_into(self, pa, sa, pb, sb, n):
         self.d.merge_into(pa, sa, pb, sb, n)
+
+    def merge_forests(self, stack, n):
+        return self.d.merge_forests(stack, n)
+
+    def now(self):
+        import time
+
+        torch.cuda.synchronize()
+        return time.perf_counter()

@@ -1,5 +1,6 @@
-"""The sharded pipeline (sheep_amd.dist) on CPU with gloo: world_size 2 and 3, edge shards
-as graph2tree -l i/P, degree all-reduce, partial trees, log2 pairwise reduce to rank 0.
+"""The sharded pipeline (sheep_amd.dist) on CPU with gloo: world_size 2, 3 and 4, edge shards
+as graph2tree -l i/P, degree all-reduce, partial trees, pst sum-reduce + parent gather to
+rank 0 and one P-way forest merge.
 The per-rank kernels are the CPU checker here (test-only backend); the orchestration and the
 collectives are the product code."""
 import os
@@ -32,6 +33,18 @@ class CheckerOps:
     def build_tree(self, uv, rmap, seq, n_seq, deg_local, selfc, mode):
         p, s = self.O.build_tree(uv.numpy(), self.seq)
         return torch.from_numpy(p.copy()), torch.from_numpy(s.copy())
+
+    def merge_forests(self, stack, n):
+        z = np.zeros(n, np.uint32)
+        p = stack[0].numpy().copy()
+        for r in range(1, stack.shape[0]):
+            p, _ = self.O.merge(p, z, stack[r].numpy().copy(), z)
+        return torch.from_numpy(np.ascontiguousarray(p))
+
+    def now(self):
+        import time
+
+        return time.perf_counter()
 
     def merge_into(self, pa, sa, pb, sb, n):
         p, s = self.O.merge(pa.numpy(), sa.numpy(), pb.numpy(), sb.numpy())

@@ -209,8 +209,10 @@ def test_sharded_partial_trees_with_degree_pst(oracle, gpu, seed):
     oseq = oracle.degree_sequence(uv)
     assert n_seq == len(oseq) and np.array_equal(seq[:n_seq].cpu().numpy().view(np.uint32), oseq)
     acc = None
+    parts = []
     for r, (sh, d, sc) in enumerate(shards):
         p, s = device.build_tree_deg(sh, rank, seq, n_seq, d, sc)
+        parts.append(p[:n_seq].clone())
         op, os_ = oracle.build_tree(uv[R * r // P: R * (r + 1) // P], oseq)
         assert np.array_equal(p[:n_seq].cpu().numpy().view(np.uint32), op)
         assert np.array_equal(s[:n_seq].cpu().numpy().view(np.uint32), os_)
@@ -222,6 +224,34 @@ def test_sharded_partial_trees_with_degree_pst(oracle, gpu, seed):
     wp, ws = oracle.build_tree(uv, oseq)
     assert np.array_equal(acc[0][:n_seq].cpu().numpy().view(np.uint32), wp)
     assert np.array_equal(acc[1][:n_seq].cpu().numpy().view(np.uint32), ws)
+    # the multi-GPU reduce: one P-way union build over the gathered parent arrays
+    mp = device.merge_forests(torch.stack(parts), n_seq)
+    torch.cuda.synchronize()
+    assert np.array_equal(mp[:n_seq].cpu().numpy().view(np.uint32), wp)
+
+
+@pytest.mark.parametrize("P", [1, 2, 5, 8])
+def test_merge_forests_equals_whole(oracle, gpu, P):
+    """sheep_merge_forests_dev over P partial trees (scale 14) is the whole graph's tree, and
+    the union of a forest with itself or with an empty forest is that forest."""
+    import torch
+    from sheep_amd import device
+
+    uv = oracle.rmat(14, 16, 90 + P)
+    seq = oracle.degree_sequence(uv)
+    n = len(seq)
+    R = len(uv)
+    parts = [oracle.build_tree(uv[R * r // P: R * (r + 1) // P], seq)[0] for r in range(P)]
+    stack = torch.from_numpy(np.stack(parts).view(np.int32)).cuda().view(torch.uint32)
+    got = device.merge_forests(stack, n)
+    wp, _ = oracle.build_tree(uv, seq)
+    assert np.array_equal(got[:n].cpu().numpy().view(np.uint32), wp)
+    twice = device.merge_forests(torch.stack([got[:n], got[:n]]), n)
+    empty = torch.full((n,), 0xFFFFFFFF, dtype=torch.int64).to(torch.int32).cuda().view(torch.uint32)
+    with_empty = device.merge_forests(torch.stack([empty, got[:n]]), n)
+    torch.cuda.synchronize()
+    assert np.array_equal(twice[:n].cpu().numpy().view(np.uint32), wp)
+    assert np.array_equal(with_empty[:n].cpu().numpy().view(np.uint32), wp)
 
 
 KB_KNOBS = [
