@@ -123,6 +123,18 @@ int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_
 int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_t n,
                             uint32_t* d_parent_out, void* stream);
 
+/* Partition quality of a k-way vertex partition (Partition::evaluate(graph) and
+ * evaluate(graph, seq), partition.cpp:428-521) over the m edge records in HBM, counted on
+ * LLAMA's undirected adjacency as the reference does.  d_parts: n_ids int16 parts (every id
+ * with an edge needs one in [0, n_parts)); d_rank: n_ids positions in seq (sheep_sequence_dev).
+ * out (host, 11 words): edges cut, Vcom vol, vertex balance (max), ECV(hash), its balance,
+ * ECV(down), its balance, ECV(up), its balance, edges (adjacency entries / 2), nodes.
+ * Synchronises.  -ERANGE: an id, part or position out of range; -EINVAL: n_parts outside
+ * [1, 32768] or 2m >= 2^32. */
+int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                       const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
+                       void* stream);
+
 /* The whole single-device hot path: degree -> sequence -> tree (graph2tree's Sorted+Mapped).
  * d_seq holds n_ids entries, d_parent/d_pst hold n_ids entries (n_seq used).  Synchronises. */
 int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,

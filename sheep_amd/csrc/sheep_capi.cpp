@@ -568,6 +568,47 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   API_END
 }
 
+int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                       const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
+                       void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (n_parts == 0 || n_parts > 32768) throw ApiError(-EINVAL, "n_parts must be in [1, 32768]");
+  if (2 * m >= (1ull << 32)) throw ApiError(-EINVAL, "evaluate: 2m adjacency entries must fit u32");
+  hipStream_t s = pick(c, stream);
+  uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
+  launch_degree(d_uv, m, n_ids, SHEEP_DEGREE_LLAMA, deg, nullptr, c.d_err, s);
+  uint64_t* keys = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(2 * m, 1) * 8);
+  uint64_t* keys_b = (uint64_t*)c.scratch.get("e_items_b", std::max<uint64_t>(2 * m, 1) * 8);
+  uint32_t* rtmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(2 * m) * 4);
+  const size_t wsn = 4 * (size_t)n_parts + 8;
+  unsigned long long* ws = (unsigned long long*)c.scratch.get("eval_ws", wsn * 8);
+  launch_evaluate(d_uv, m, d_parts, d_rank, deg, n_ids, n_parts, keys, keys_b, rtmp, ws, c.d_err, s);
+  std::vector<unsigned long long> h(wsn);
+  HIP_CHECK(hipMemcpyAsync(h.data(), ws, wsn * 8, hipMemcpyDeviceToHost, s));
+  check_err(c, s);  // synchronises; -ERANGE for an id, part or position out of range
+  const unsigned long long* cnt = h.data() + 4 * (size_t)n_parts;
+  auto mx = [&](size_t off) {
+    unsigned long long v = 0;
+    for (uint32_t i = 0; i < n_parts; ++i) v = std::max(v, h[off + i]);
+    return (uint64_t)v;
+  };
+  const uint64_t nodes = cnt[2];
+  out[0] = cnt[0];
+  out[1] = cnt[3];
+  out[2] = mx(3 * (size_t)n_parts);
+  out[3] = cnt[4] - nodes;
+  out[4] = mx(0);
+  out[5] = cnt[5] - nodes;
+  out[6] = mx(n_parts);
+  out[7] = cnt[6] - nodes;
+  out[8] = mx(2 * (size_t)n_parts);
+  out[9] = (2 * m - cnt[1]) / 2;
+  out[10] = nodes;
+  API_END
+}
+
 int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
                    void* stream) {
   API_BEGIN

@@ -99,6 +99,13 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      bool refresh, bool stats, unsigned long long* st, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
+// Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)
+// vertex balance, then cut, self-loop records, nodes, and the distinct keys of vcom, hash,
+// down, up.  keys/keys_b: 2m u64; rtmp: rsort_tmp_words(2m) u32; deg: LLAMA degrees.
+void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const uint32_t* pos,
+                     const uint32_t* deg, uint32_t n_ids, uint32_t k, uint64_t* keys,
+                     uint64_t* keys_b, uint32_t* rtmp, unsigned long long* ws, uint32_t* err,
+                     hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

@@ -92,6 +92,23 @@ def merge_forests(parents, n, out=None):
     return out
 
 
+EVAL_KEYS = ("edges_cut", "vcom_vol", "vertex_bal", "ecv_hash", "hash_bal", "ecv_down",
+             "down_bal", "ecv_up", "up_bal", "edges", "nodes")
+
+
+def evaluate(uv, parts, rank, n_parts=None):
+    """Partition::evaluate(graph, seq) on the GPU: ``parts`` int16 per vertex id (cuda),
+    ``rank`` the positions in seq (sheep_sequence_dev).  Returns a dict (EVAL_KEYS)."""
+    import numpy as np
+
+    if n_parts is None:
+        n_parts = int(parts.max().item()) + 1
+    out = np.zeros(11, np.uint64)
+    capi.call("sheep_evaluate_dev", _p(uv), uv.shape[0], _p(parts), _p(rank), parts.numel(),
+              n_parts, ctypes.c_void_p(out.ctypes.data), _stream())
+    return dict(zip(EVAL_KEYS, (int(x) for x in out)))
+
+
 def graph2tree(uv, n_ids, mode=capi.DEGREE_LLAMA, seq=None, parent=None, pst=None):
     dev = uv.device
     seq = seq if seq is not None else torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev)
