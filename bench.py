@@ -39,12 +39,12 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def pmc_traffic(kernel, scale):
+def pmc_traffic(kernel, key):
     """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/), if one was
     collected for this workload: FETCH_SIZE and WRITE_SIZE from separate rocprofv3 --pmc passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        tab = json.load(open(path))["rmat%d" % scale]
+        tab = json.load(open(path))[key]
         rec = tab.get(kernel) or tab["sheep::" + kernel]
         return rec["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="rmat", choices=["rmat", "lj", "twitter"],
+                    help="rmat: Graph500 R-MAT (--scale); lj / twitter: the power-law configs "
+                         "C3 / C5 of BASELINE.json")
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=26)
@@ -93,10 +96,22 @@ def main():
 
     device.init(local)
     scale, ef, seed = args.scale, args.edgefactor, args.seed
-    m = ef << scale
-    n_ids = 1 << scale
-    lo, hi = shard_bounds(m, rank, world)
-    uv = device.rmat(scale, ef, seed, lo, hi)  # this rank's records, resident in HBM
+    if args.workload == "rmat":
+        m = ef << scale
+        n_ids = 1 << scale
+        lo, hi = shard_bounds(m, rank, world)
+        uv = device.rmat(scale, ef, seed, lo, hi)  # this rank's records, resident in HBM
+        wl = {"workload": "rmat%d_ef%d" % (scale, ef), "scale": scale, "edgefactor": ef,
+              "seed": seed}
+        data = "synthetic R-MAT (Graph500 A/B/C/D .57/.19/.19/.05), generated in HBM"
+    else:
+        n_ids, m, gamma, i0, seed = device.POWERLAW[args.workload]
+        lo, hi = shard_bounds(m, rank, world)
+        uv = device.powerlaw(n_ids, m, gamma, i0, seed, lo, hi)
+        wl = {"workload": "%s_shape_powerlaw" % args.workload, "gamma": gamma, "i0": i0,
+              "seed": seed}
+        data = ("synthetic power-law (Chung-Lu, P(i) ~ (i+%g)^-1/(%g-1)), %s-shape n and m, "
+                "generated in HBM" % (i0, gamma, args.workload))
     torch.cuda.synchronize()
     ops = DeviceOps()
 
@@ -141,25 +156,28 @@ def main():
             ach = algo / (avg["edge_pass"] * 1e-3)
             roof = {"kernel": "k_edge_pass", "bound": "hbm", "achieved": ach / 1e9,
                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
-                    "traffic": pmc_traffic("k_edge_pass", scale), "algo_bytes": algo,
+                    "traffic": pmc_traffic("k_edge_pass", "rmat%d" % scale
+                                           if args.workload == "rmat" else args.workload),
+                    "algo_bytes": algo,
                     "avg_ms": avg["edge_pass"],
                     "phases_ms": {k: round(v, 3) for k, v in avg.items()}}
         path_bytes = 16 * m + 24 * n_seq  # SURVEY §8d B(m, n)
+        label = "RMAT-%d" % scale if args.workload == "rmat" else wl["workload"]
         rec = {
-            "metric": "edges/sec to build elimination tree (RMAT-%d)" % scale,
+            "metric": "edges/sec to build elimination tree (%s)" % label,
             "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic R-MAT (Graph500 A/B/C/D .57/.19/.19/.05), generated in HBM",
-            "config": {"workload": "rmat%d_ef%d" % (scale, ef), "scale": scale, "edgefactor": ef,
-                       "seed": seed, "records": m, "n_ids": n_ids, "n_seq": n_seq,
-                       "parallelism": "edge-shard x%d" % world if world > 1 else "single"},
+            "data": data,
+            "config": dict(wl, records=m, n_ids=n_ids, n_seq=n_seq,
+                           parallelism="edge-shard x%d" % world if world > 1 else "single"),
             "path_roofline": {"bytes": path_bytes,
                               "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK)},
             "roofline": roof,
         }
         if args.check:
-            rec["check"] = check_tree(out, scale, ef, seed)
+            rec["check"] = check_tree(out, uv if world == 1 else None, scale, ef, seed,
+                                      args.workload)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef, args.cpu_scale)
         print(json.dumps(rec), flush=True)
@@ -167,12 +185,16 @@ def main():
         dist.destroy_process_group()
 
 
-def check_tree(out, scale, ef, seed):
+def check_tree(out, uv_d, scale, ef, seed, workload):
     from oracle import oracle as O
     import numpy as np
+    from sheep_amd import device
 
     seq_d, parent_d, pst_d, n = out[0], out[1], out[2], out[3]
-    uv = O.rmat(scale, ef, seed)
+    if workload == "rmat":
+        uv = O.rmat(scale, ef, seed)
+    else:
+        uv = O.powerlaw(*device.POWERLAW[workload])
     seq = O.degree_sequence(uv)
     p, s = O.build_tree(uv, seq)
     ok = (n == len(seq)

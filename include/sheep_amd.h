@@ -146,6 +146,13 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
 int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
                    void* stream);
 
+/* Power-law (Chung-Lu style) synthetic records [e_begin, e_end) for the LiveJournal- and
+ * twitter-shape configs: endpoints drawn with P(i) ~ (i + i0)^(-1/(gamma-1)) over n ids, then
+ * relabelled by a seeded bijection.  Bit-identical to sheep_amd/csrc/powerlaw.h on the host.
+ * Enqueue only. */
+int sheep_powerlaw_dev(uint32_t* d_uv, uint32_t n, double gamma, double i0, uint64_t seed,
+                       uint64_t e_begin, uint64_t e_end, void* stream);
+
 /* Kernel timing of the last synchronising call (ms per named phase), for bench/profiling.
  * Fills up to cap (name, ms) pairs; returns the count. */
 int sheep_last_timings(const char** names, double* ms, int cap);

@@ -50,6 +50,8 @@ def lib():
             "orc_time_graph2tree": (c.c_int, [_u32p, c.c_uint64, c.c_uint32,
                                               np.ctypeslib.ndpointer(np.float64)]),
             "orc_rmat": (None, [c.c_int, c.c_uint64, c.c_uint64, c.c_uint64, _u32p]),
+            "orc_powerlaw": (None, [c.c_uint32, c.c_double, c.c_double, c.c_uint64, c.c_uint64,
+                                    c.c_uint64, _u32p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -168,6 +170,15 @@ def evaluate(uv, parts, seq):
     if r != 0:
         raise ValueError("evaluate: vertex without part")
     return dict(zip(EVAL_KEYS, (int(x) for x in out[:11])))
+
+
+def powerlaw(n, m, gamma, i0, seed, e_begin=0, e_end=None):
+    """Power-law records [e_begin, e_end) (see sheep_amd/csrc/powerlaw.h)."""
+    if e_end is None:
+        e_end = m
+    uv = np.zeros(2 * (e_end - e_begin), np.uint32)
+    lib().orc_powerlaw(n, gamma, i0, seed, e_begin, e_end, uv)
+    return uv.reshape(-1, 2)
 
 
 def rmat(scale, edgefactor, seed, e_begin=0, e_end=None):

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../sheep_amd/csrc/rmat.h"  // the build's synthetic-input definition (not reference code)
+#include "../sheep_amd/csrc/powerlaw.h"  // likewise, the power-law configs
 
 typedef uint32_t vid_t;   // defs.h:76
 typedef uint32_t jnid_t;  // jnode.h:42
@@ -459,6 +460,13 @@ int orc_time_graph2tree(const uint32_t* uv, uint64_t m, uint32_t n_ids, double* 
 
 // Synthetic R-MAT edges [e_begin, e_end) of the stream (scale, seed); see rmat.h.  Used by the
 // tests to regenerate on the host exactly what the GPU generator wrote into HBM.
+void orc_powerlaw(uint32_t n, double gamma, double i0, uint64_t seed, uint64_t e_begin,
+                  uint64_t e_end, uint32_t* uv) {
+  const sheep_pl::Table t = sheep_pl::powerlaw_table(n, gamma, i0);
+  for (uint64_t e = e_begin; e < e_end; ++e)
+    sheep_pl::edge(t, e, seed, &uv[2 * (e - e_begin)], &uv[2 * (e - e_begin) + 1]);
+}
+
 void orc_rmat(int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end, uint32_t* uv) {
   for (uint64_t e = e_begin; e < e_end; ++e)
     sheep_rmat::edge(e, scale, seed, &uv[2 * (e - e_begin)], &uv[2 * (e - e_begin) + 1]);

@@ -71,6 +71,8 @@ def lib():
         "sheep_graph2tree_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, u32p, u32p,
                                  vp],
         "sheep_rmat_dev": [u32p, c.c_int, c.c_uint64, c.c_uint64, c.c_uint64, vp],
+        "sheep_powerlaw_dev": [u32p, c.c_uint32, c.c_double, c.c_double, c.c_uint64, c.c_uint64,
+                               c.c_uint64, vp],
         "sheep_last_timings": [c.c_void_p, c.c_void_p, c.c_int],
     }
     for name, args in sigs.items():

@@ -202,8 +202,13 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   } else {
     const char* ek = getenv("SHEEP_KB_BUCKETS");
     const char* er = getenv("SHEEP_KB_RANKB");
-    uint32_t K_e = ek ? (uint32_t)atoi(ek) : 64;
-    uint32_t K_r = er ? (uint32_t)atoi(er) : 64;
+    // Bucket counts grow with the input: each bucket costs a fixed ~60-100 us of launches and
+    // small kernels, while too few buckets leave the zipper long in-bucket walks.  Measured
+    // (profiles/r01/kb_bucket_sweep.txt): LJ-shape (69M records) is best at 8 + 8, R-MAT-26
+    // (1.07G) and twitter-shape (1.47G) at 64 + 64.
+    const uint32_t K_auto = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, m >> 23));
+    uint32_t K_e = ek ? (uint32_t)atoi(ek) : K_auto;
+    uint32_t K_r = er ? (uint32_t)atoi(er) : K_auto;
     uint32_t K = K_e + K_r;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
@@ -616,6 +621,16 @@ int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, u
   require_aligned(d_uv, "d_uv");
   if (scale < 1 || scale > 32) throw ApiError(-EINVAL, "scale must be in [1, 32]");
   launch_rmat(d_uv, scale, seed, e_begin, e_end, pick(c, stream));
+  API_END
+}
+
+int sheep_powerlaw_dev(uint32_t* d_uv, uint32_t n, double gamma, double i0, uint64_t seed,
+                       uint64_t e_begin, uint64_t e_end, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (n == 0 || !(gamma > 1.0) || !(i0 >= 0.0)) throw ApiError(-EINVAL, "powerlaw: n > 0, gamma > 1, i0 >= 0");
+  launch_powerlaw(d_uv, n, gamma, i0, seed, e_begin, e_end, pick(c, stream));
   API_END
 }
 

@@ -110,5 +110,7 @@ void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,
                  hipStream_t s);
+void launch_powerlaw(uint32_t* uv, uint32_t n, double gamma, double i0, uint64_t seed,
+                     uint64_t e_begin, uint64_t e_end, hipStream_t s);
 
 }  // namespace sheep

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 
+#include "powerlaw.h"
 #include "rmat.h"
 #include "sheep_internal.h"
 
@@ -1714,6 +1715,24 @@ __global__ void k_rmat(uint2* __restrict__ uv, int scale, uint64_t seed, uint64_
     sheep_rmat::edge(e_begin + i, scale, seed, &t, &h);
     uv[i] = make_uint2(t, h);
   }
+}
+
+__global__ void k_powerlaw(uint2* __restrict__ uv, sheep_pl::Table t, uint64_t seed,
+                           uint64_t e_begin, uint64_t n) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t a, b;
+    sheep_pl::edge(t, e_begin + i, seed, &a, &b);
+    uv[i] = make_uint2(a, b);
+  }
+}
+
+void launch_powerlaw(uint32_t* uv, uint32_t n, double gamma, double i0, uint64_t seed,
+                     uint64_t e_begin, uint64_t e_end, hipStream_t s) {
+  if (e_end <= e_begin) return;
+  const sheep_pl::Table t = sheep_pl::powerlaw_table(n, gamma, i0);
+  hipLaunchKernelGGL(k_powerlaw, dim3(grid_for(e_end - e_begin)), dim3(BLOCK), 0, s, (uint2*)uv, t,
+                     seed, e_begin, e_end - e_begin);
 }
 
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

@@ -32,6 +32,23 @@ def rmat(scale, edgefactor, seed, e_begin=0, e_end=None, device="cuda"):
     return uv
 
 
+# Power-law workloads (BASELINE.json configs C3, C5): (n ids, m records, gamma, i0, seed)
+POWERLAW = {
+    "lj": (4847571, 68993773, 2.3, 100.0, 3),
+    "twitter": (41652230, 1468365182, 2.1, 50.0, 5),
+}
+
+
+def powerlaw(n, m, gamma, i0, seed, e_begin=0, e_end=None, device="cuda"):
+    """Power-law records [e_begin, e_end) of the (n, gamma, i0, seed) stream, (k, 2) uint32."""
+    if e_end is None:
+        e_end = m
+    uv = torch.empty((e_end - e_begin, 2), dtype=torch.uint32, device=device)
+    capi.call("sheep_powerlaw_dev", _p(uv), n, float(gamma), float(i0), seed, e_begin, e_end,
+              _stream())
+    return uv
+
+
 def degree(uv, n_ids, mode=capi.DEGREE_LLAMA, out=None):
     deg = out if out is not None else torch.empty(n_ids, dtype=torch.uint32, device=uv.device)
     capi.call("sheep_degree_dev", _p(uv), uv.shape[0], n_ids, mode, _p(deg), _stream())

@@ -80,6 +80,31 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("n,m,gamma,i0,seed", [(1000, 20000, 2.3, 100.0, 3),
+                                               (65536, 1 << 20, 2.1, 50.0, 5),
+                                               (300001, 1 << 21, 2.3, 100.0, 7)])
+def test_powerlaw_generator_and_tree(oracle, api, gpu, n, m, gamma, i0, seed):
+    """The LJ/twitter-shape generator: the GPU stream equals the host stream (any slice), and
+    the tree of a power-law graph (hubs, isolated ids, self-loops) is bit-exact."""
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.powerlaw(n, m, gamma, i0, seed)
+    uv = uv_d.cpu().numpy().view(np.uint32)
+    assert np.array_equal(uv, oracle.powerlaw(n, m, gamma, i0, seed))
+    part = device.powerlaw(n, m, gamma, i0, seed, m // 3, m // 2).cpu().numpy().view(np.uint32)
+    assert np.array_equal(part, uv[m // 3: m // 2])
+    assert uv.max() < n
+    s_d, p_d, w_d, k = device.graph2tree(uv_d, n)
+    torch.cuda.synchronize()
+    seq = oracle.degree_sequence(uv)
+    p, w = oracle.build_tree(uv, seq)
+    assert k == len(seq)
+    assert np.array_equal(s_d[:k].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:k].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_multigraphs(oracle, api, seed):
     rng = np.random.default_rng(100 + seed)

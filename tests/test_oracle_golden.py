@@ -123,3 +123,16 @@ def test_oracle_merge_of_shards_equals_whole(oracle):
         for t in trees[1:]:
             acc = oracle.merge(acc[0], acc[1], t[0], t[1])
         assert np.array_equal(acc[0], whole[0]) and np.array_equal(acc[1], whole[1])
+
+
+def test_powerlaw_stream_is_sliceable_and_heavy_tailed(oracle):
+    """The power-law generator (sheep_amd/csrc/powerlaw.h, host side): slices concatenate to
+    the stream, ids stay in [0, n), and the degree distribution has a hub head and a long tail."""
+    n, m = 50000, 400000
+    uv = oracle.powerlaw(n, m, 2.3, 100.0, 3)
+    assert uv.shape == (m, 2) and uv.max() < n
+    assert np.array_equal(np.concatenate([oracle.powerlaw(n, m, 2.3, 100.0, 3, 0, 1234),
+                                          oracle.powerlaw(n, m, 2.3, 100.0, 3, 1234, m)]), uv)
+    deg = np.bincount(uv.ravel(), minlength=n)
+    assert deg.max() > 30 * deg.mean()          # hubs
+    assert np.median(deg) < 0.7 * deg.mean()    # most ids below the mean: a long tail
