@@ -45,10 +45,12 @@ def pmc_traffic(kernel, key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         tab = json.load(open(path))[key]
-        rec = tab.get(kernel) or tab["sheep::" + kernel]
-        return rec["hbm_bytes_per_launch"]
+        for k, rec in tab.items():
+            if k.replace("sheep::", "").split("<")[0] == kernel:
+                return rec["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
-        return None
+        pass
+    return None
 
 
 def cpu_baseline(scale, edgefactor, seed):
@@ -146,21 +148,34 @@ def main():
         ms_per_step = 1e3 * elapsed / args.steps
         n_seq = out[3] if world > 1 else out[3]
         value = m / (elapsed / args.steps)
-        # Roofline of the dominant single kernel, k_edge_pass (one launch per step; its phase
-        # is bracketed by HIP events on the stream it runs on).  Algorithmic bytes per launch
-        # (DESIGN.md §5): 8 B record read + 8 B item written + 2 x 4 B rank words gathered.
+        # Roofline of the dominant kernel: the one with the most time per step among those
+        # bracketed live by HIP events on the stream they run on:
+        #   k_kb_map (one launch per bucket, side stream): 8 B per record streamed + 4 B per
+        #     rank of hi counts; its union-find / label gathers are not algorithmic bytes;
+        #   k_edge_pass (one launch): 8 B record read + 8 B item written + 2 x 4 B rank words.
         avg = {k: sum(v) / len(v) for k, v in phase.items()}
-        roof = None
+        recs = hi - lo if world > 1 else m
+        key = "rmat%d" % scale if args.workload == "rmat" else args.workload
+        cands = []
         if "edge_pass" in avg:
-            algo = 24 * (hi - lo) if world > 1 else 24 * m
-            ach = algo / (avg["edge_pass"] * 1e-3)
-            roof = {"kernel": "k_edge_pass", "bound": "hbm", "achieved": ach / 1e9,
+            cands.append(("k_edge_pass_tiles", avg["edge_pass"], 1, 24 * recs))
+        if avg.get("kb_map#"):
+            cands.append(("k_kb_map", avg["kb_map"], avg["kb_map#"], 8 * recs + 4 * n_seq))
+        roof = None
+        if cands:
+            name, ms, launches, algo = max(cands, key=lambda c: c[1])
+            per_launch_ms = ms / launches
+            ach = (algo / launches) / (per_launch_ms * 1e-3)
+            roof = {"kernel": name, "bound": "hbm", "achieved": ach / 1e9,
                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
-                    "traffic": pmc_traffic("k_edge_pass", "rmat%d" % scale
-                                           if args.workload == "rmat" else args.workload),
-                    "algo_bytes": algo,
-                    "avg_ms": avg["edge_pass"],
-                    "phases_ms": {k: round(v, 3) for k, v in avg.items()}}
+                    "traffic": pmc_traffic(name, key), "algo_bytes": algo / launches,
+                    "avg_ms": per_launch_ms, "launches_per_step": launches,
+                    "ms_per_step": ms,
+                    "phases_ms": {k: round(v, 3) for k, v in avg.items() if not k.endswith("#")},
+                    "others": {c[0]: {"ms_per_step": round(c[1], 3),
+                                      "GB_s": round(c[3] / (c[1] * 1e-3) / 1e9, 1),
+                                      "traffic_per_launch": pmc_traffic(c[0], key)}
+                               for c in cands if c[0] != name}}
         path_bytes = 16 * m + 24 * n_seq  # SURVEY §8d B(m, n)
         label = "RMAT-%d" % scale if args.workload == "rmat" else wl["workload"]
         rec = {

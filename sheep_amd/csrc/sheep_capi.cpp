@@ -12,6 +12,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/sheep_amd.h"
@@ -111,16 +112,48 @@ struct Timer {
     HIP_CHECK(hipEventRecord(e, s));
     ev.emplace_back(name, e);
   }
+  // Kernel spans on any stream (events right before and after one launch), summed per name
+  // in finish(): "<name>" = total ms, "<name>#" = launches.
+  std::vector<std::tuple<const char*, hipEvent_t, hipEvent_t>> spans;
+  size_t span_begin(const char* name, hipStream_t st) {
+    hipEvent_t a, b;
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&b));
+    HIP_CHECK(hipEventRecord(a, st));
+    spans.emplace_back(name, a, b);
+    return spans.size() - 1;
+  }
+  void span_end(size_t i, hipStream_t st) { HIP_CHECK(hipEventRecord(std::get<2>(spans[i]), st)); }
   void finish(Ctx& c) {  // after the stream has been synchronised
     c.timings.clear();
+    c.span_names.clear();
     for (size_t i = 1; i < ev.size(); ++i) {
       float ms = 0;
       (void)hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second);
       c.timings.emplace_back(ev[i].first, (double)ms);
     }
+    std::vector<std::pair<const char*, std::pair<double, double>>> sums;
+    for (auto& sp : spans) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, std::get<1>(sp), std::get<2>(sp));
+      size_t j = 0;
+      while (j < sums.size() && strcmp(sums[j].first, std::get<0>(sp))) ++j;
+      if (j == sums.size()) sums.push_back({std::get<0>(sp), {0.0, 0.0}});
+      sums[j].second.first += ms;
+      sums[j].second.second += 1;
+    }
+    for (auto& x : sums) {
+      c.timings.emplace_back(x.first, x.second.first);
+      c.span_names.push_back(std::string(x.first) + "#");
+      c.timings.emplace_back(c.span_names.back().c_str(), x.second.second);
+    }
   }
   ~Timer() {
     for (auto& e : ev) (void)hipEventDestroy(e.second);
+    for (auto& sp : spans) {
+      (void)hipEventDestroy(std::get<1>(sp));
+      (void)hipEventDestroy(std::get<2>(sp));
+    }
   }
 };
 
@@ -260,8 +293,10 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     };
     auto map_k = [&](size_t k, hipStream_t st) {
       int p = par(k);
+      size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
       launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
                     kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws, st);
+      if (tm) tm->span_end(sp, st);
     };
     auto apply_k = [&](size_t k, hipStream_t st) {
       int p = par(k);

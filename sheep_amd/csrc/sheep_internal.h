@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -33,6 +34,7 @@ struct Ctx {
   uint32_t* d_err = nullptr;     // device error word
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
   std::vector<std::pair<const char*, double>> timings;
+  std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
 };
 
 Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)
