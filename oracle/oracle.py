@@ -49,6 +49,8 @@ def lib():
                                        _u64p]),
             "orc_time_graph2tree": (c.c_int, [_u32p, c.c_uint64, c.c_uint32,
                                               np.ctypeslib.ndpointer(np.float64)]),
+            "orc_time_graph2tree_ir": (c.c_int, [_u32p, c.c_uint64, c.c_uint32, c.c_int,
+                                                 np.ctypeslib.ndpointer(np.float64)]),
             "orc_rmat": (None, [c.c_int, c.c_uint64, c.c_uint64, c.c_uint64, _u32p]),
             "orc_powerlaw": (None, [c.c_uint32, c.c_double, c.c_double, c.c_uint64, c.c_uint64,
                                     c.c_uint64, _u32p]),
@@ -196,3 +198,12 @@ def time_graph2tree(uv, n_ids):
     out = np.zeros(3, np.float64)
     lib().orc_time_graph2tree(uv.reshape(-1), uv.size // 2, n_ids, out)
     return float(out[0]), float(out[1]), int(out[2])
+
+
+def time_graph2tree_ir(uv, n_ids, threads):
+    """`mpirun -n threads graph2tree -ir` analogue on threads: (sort_s, map_s, reduce_s, n_seq,
+    result equals the serial tree)."""
+    uv = np.ascontiguousarray(uv, np.uint32)
+    out = np.zeros(5, np.float64)
+    lib().orc_time_graph2tree_ir(uv.reshape(-1), uv.size // 2, n_ids, threads, out)
+    return out[0], out[1], out[2], int(out[3]), bool(out[4])

@@ -27,6 +27,7 @@
 #include <fstream>
 #include <numeric>
 #include <unordered_set>
+#include <thread>
 #include <vector>
 
 #include "../sheep_amd/csrc/rmat.h"  // the build's synthetic-input definition (not reference code)
@@ -455,6 +456,110 @@ int orc_time_graph2tree(const uint32_t* uv, uint64_t m, uint32_t n_ids, double* 
   out[2] = n;
   volatile uint32_t sink = parent.empty() ? 0 : parent[n / 2];
   (void)sink;
+  return 0;
+}
+
+// The `mpirun -n T graph2tree -ir` analogue (graph2tree.cpp:134-200) on T threads, the
+// reference's multi-core CPU path, for bench.py's cpu_baseline: T contiguous record shards
+// (-l i/T, graph_wrapper.h:48-49), each loaded as its own CSR (untimed, as LLAMA's load);
+// timed: "Sorted" = shard degrees + their sum (mpiSequence's MPI_Allreduce, sequence.h:65-93)
+// + the (deg, id) sort; "Mapped" = each shard's JTree on its thread (jtree.cpp:112-145);
+// "Reduced" = the partial trees merged pairwise in log2(T) rounds, the pairs of a round on
+// parallel threads (mpi_merge's reduce tree, jnode.cpp:203-250).  Checks that the result is
+// the serial tree's.  out = {sort_s, map_s, reduce_s, n_seq, ok}.
+int orc_time_graph2tree_ir(const uint32_t* uv, uint64_t m, uint32_t n_ids, int T, double* out) {
+  if (T < 1) T = 1;
+  std::vector<CSR> g(T);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        uint64_t lo = m * t / T, hi = m * (t + 1) / T;
+        g[t] = build_csr(uv + 2 * lo, hi - lo, n_ids);
+      });
+    for (auto& x : th) x.join();
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  // Sorted: degrees of every shard, summed by id range on the T threads, then the sort
+  std::vector<uint32_t> deg(n_ids, 0);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        uint64_t lo = (uint64_t)n_ids * t / T, hi = (uint64_t)n_ids * (t + 1) / T;
+        for (int s = 0; s < T; ++s)
+          for (uint64_t v = lo; v < hi; ++v) deg[v] += (uint32_t)(g[s].off[v + 1] - g[s].off[v]);
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<uint32_t> seq;
+  seq.reserve(n_ids);
+  for (uint32_t v = 0; v < n_ids; ++v)
+    if (deg[v]) seq.push_back(v);
+  auto less = [&deg](uint32_t a, uint32_t b) { return deg[a] != deg[b] ? deg[a] < deg[b] : a < b; };
+  {  // T sorted runs, then pairwise merges (what __gnu_parallel::sort does with T threads)
+    std::vector<size_t> cut(T + 1);
+    for (int t = 0; t <= T; ++t) cut[t] = seq.size() * t / T;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] { std::sort(seq.begin() + cut[t], seq.begin() + cut[t + 1], less); });
+    for (auto& x : th) x.join();
+    for (int w = 1; w < T; w *= 2) {
+      std::vector<std::thread> mt;
+      for (int t = 0; t + w < T; t += 2 * w)
+        mt.emplace_back([&, t, w] {
+          size_t e = cut[std::min(T, t + 2 * w)];
+          std::inplace_merge(seq.begin() + cut[t], seq.begin() + cut[t + w], seq.begin() + e, less);
+        });
+      for (auto& x : mt) x.join();
+    }
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  const uint32_t n = (uint32_t)seq.size();
+  std::vector<std::vector<uint32_t>> par(T, std::vector<uint32_t>(n)), ps(T, std::vector<uint32_t>(n));
+  {
+    std::vector<uint32_t> index(n_ids, INVALID);
+    for (uint32_t i = 0; i < n; ++i) index[seq[i]] = i;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        UF uf(n);
+        uint32_t* parent = par[t].data();
+        uint32_t* pst = ps[t].data();
+        const CSR& c = g[t];
+        for (uint32_t cur = 0; cur < n; ++cur) {
+          uint32_t X = seq[cur];
+          parent[cur] = INVALID;
+          pst[cur] = 0;
+          for (uint64_t k = c.off[X]; k < c.off[X + 1]; ++k) {
+            uint32_t nb = c.adj[k], nid = index[nb];
+            if (nid < cur) adopt(uf, parent, nid, cur);
+            else if (nid != cur) ++pst[cur];
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  for (int w = 1; w < T; w *= 2) {
+    std::vector<std::thread> th;
+    for (int t = 0; t + w < T; t += 2 * w)
+      th.emplace_back([&, t, w] {
+        std::vector<uint32_t> p(n), q(n);
+        orc_merge(par[t].data(), ps[t].data(), par[t + w].data(), ps[t + w].data(), n, p.data(), q.data());
+        par[t].swap(p);
+        ps[t].swap(q);
+      });
+    for (auto& x : th) x.join();
+  }
+  auto t3 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> sp(n), ss(n);
+  int ok = orc_build_tree(uv, m, seq.data(), n, sp.data(), ss.data()) == 0 && sp == par[0] && ss == ps[0];
+  out[0] = std::chrono::duration<double>(t1 - t0).count();
+  out[1] = std::chrono::duration<double>(t2 - t1).count();
+  out[2] = std::chrono::duration<double>(t3 - t2).count();
+  out[3] = n;
+  out[4] = ok;
   return 0;
 }
 

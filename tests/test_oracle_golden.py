@@ -136,3 +136,12 @@ def test_powerlaw_stream_is_sliceable_and_heavy_tailed(oracle):
     deg = np.bincount(uv.ravel(), minlength=n)
     assert deg.max() > 30 * deg.mean()          # hubs
     assert np.median(deg) < 0.7 * deg.mean()    # most ids below the mean: a long tail
+
+
+def test_ir_analogue_equals_serial_tree(oracle):
+    """The `graph2tree -ir` CPU baseline (T shards, per-shard trees, log2(T) merge reduce) builds
+    the serial tree (its own check flag), for T not a power of two too."""
+    uv = oracle.rmat(12, 16, 9)
+    for T in (1, 3, 4):
+        _, _, _, n, ok = oracle.time_graph2tree_ir(uv, 1 << 12, T)
+        assert ok and n == len(oracle.degree_sequence(uv))
