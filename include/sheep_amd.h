@@ -135,6 +135,12 @@ int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
                        const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
                        void* stream);
 
+/* Host-pointer sheep_evaluate_dev, as Partition::evaluate(graph, seq) calls it: parts are
+ * n_parts_vid int16 per vertex id (ids beyond it have no part), seq the n_seq ids in sequence
+ * order.  Uploads, evaluates, synchronises. */
+int sheep_evaluate(const uint32_t* edges_uv, uint64_t m, const int16_t* parts, uint32_t n_parts_vid,
+                   const uint32_t* seq, uint32_t n_seq, uint32_t n_parts, uint64_t* out);
+
 /* The whole single-device hot path: degree -> sequence -> tree (graph2tree's Sorted+Mapped).
  * d_seq holds n_ids entries, d_parent/d_pst hold n_ids entries (n_seq used).  Synchronises. */
 int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,

@@ -68,6 +68,7 @@ def lib():
         "sheep_merge_trees_dev": [u32p, u32p, u32p, u32p, c.c_uint32, vp],
         "sheep_merge_forests_dev": [u32p, c.c_uint32, c.c_uint32, u32p, vp],
         "sheep_evaluate_dev": [u32p, c.c_uint64, vp, u32p, c.c_uint32, c.c_uint32, vp, vp],
+        "sheep_evaluate": [u32p, c.c_uint64, vp, c.c_uint32, u32p, c.c_uint32, c.c_uint32, vp],
         "sheep_graph2tree_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, u32p, u32p,
                                  vp],
         "sheep_rmat_dev": [u32p, c.c_int, c.c_uint64, c.c_uint64, c.c_uint64, vp],

@@ -608,15 +608,11 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   API_END
 }
 
-int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
-                       const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
-                       void* stream) {
-  API_BEGIN
-  Ctx& c = ctx();
-  require_aligned(d_uv, "d_uv");
+static void evaluate_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                         const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
+                         hipStream_t s) {
   if (n_parts == 0 || n_parts > 32768) throw ApiError(-EINVAL, "n_parts must be in [1, 32768]");
   if (2 * m >= (1ull << 32)) throw ApiError(-EINVAL, "evaluate: 2m adjacency entries must fit u32");
-  hipStream_t s = pick(c, stream);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
   launch_degree(d_uv, m, n_ids, SHEEP_DEGREE_LLAMA, deg, nullptr, c.d_err, s);
   uint64_t* keys = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(2 * m, 1) * 8);
@@ -646,6 +642,15 @@ int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
   out[8] = mx(2 * (size_t)n_parts);
   out[9] = (2 * m - cnt[1]) / 2;
   out[10] = nodes;
+}
+
+int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                       const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
+                       void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  evaluate_dev(c, d_uv, m, d_parts, d_rank, n_ids, n_parts, out, pick(c, stream));
   API_END
 }
 
@@ -693,6 +698,30 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
     HIP_CHECK(hipMemcpyAsync(rank_out, rank, (size_t)n_ids * 4, hipMemcpyDeviceToHost, s));
   check_err(c, s);
   if (n_seq_out) *n_seq_out = n_seq;
+  API_END
+}
+
+int sheep_evaluate(const uint32_t* edges_uv, uint64_t m, const int16_t* parts, uint32_t n_parts_vid,
+                   const uint32_t* seq, uint32_t n_seq, uint32_t n_parts, uint64_t* out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = c.stream;
+  uint32_t n_ids = n_parts_vid;
+  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
+  for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
+  HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));  // INVALID_PART = -1
+  if (n_parts_vid)
+    HIP_CHECK(hipMemcpyAsync(dparts, parts, (size_t)n_parts_vid * 2, hipMemcpyHostToDevice, s));
+  uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)std::max<uint32_t>(n_seq, 1) * 4);
+  if (n_seq) HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
+  launch_fill(rank, INV, n_ids, s);
+  launch_rank_scatter(dseq, n_seq, rank, c.d_err, s);
+  check_err(c, s);
+  evaluate_dev(c, uv, m, dparts, rank, n_ids, n_parts, out, s);
   API_END
 }
 

@@ -19,6 +19,7 @@
 #include "defs.h"
 #include "graph_wrapper.h"
 #include "jnode.h"
+#include "sheep_call.h"
 #include "readerwriter.h"
 
 class Partition {
@@ -164,6 +165,29 @@ class Partition {
     printf("  balance: %zu (%f%%)\n", mdb, (double)mdb / (graph.getEdges() / num_parts));
     printf("ECV(up)  : %zu (%f%%)\n", ECV_up, (double)ECV_up / graph.getEdges());
     printf("  balance: %zu (%f%%)\n", mub, (double)mub / (graph.getEdges() / num_parts));
+  }
+
+  // evaluate(graph) + evaluate(graph, seq) in one call on the GPU (sheep_evaluate, the MI355X
+  // path for big graphs): the same numbers and the same printed lines as the two host loops
+  // above, which walk an unordered_set per vertex.  partition_tree -G selects it.
+  template <typename GraphType>
+  void evaluate_gpu(GraphType const& graph, std::vector<vid_t> const& seq) const {
+    uint64_t o[11];
+    part_t max_part = *std::max_element(parts.cbegin(), parts.cend());
+    sheep_check(sheep_evaluate(graph.records_data(), graph.records(), parts.data(),
+                               (uint32_t)parts.size(), seq.data(), (uint32_t)seq.size(),
+                               (uint32_t)max_part + 1, o),
+                "Partition::evaluate");
+    const double E = (double)graph.getEdges();
+    printf("edges cut: %zu (%f%%)\n", (size_t)o[0], (double)o[0] / E);
+    printf("Vcom. vol: %zu (%f%%)\n", (size_t)o[1], (double)o[1] / E);
+    printf("  balance: %zu (%f%%)\n", (size_t)o[2], (double)o[2] / (graph.getNodes() / num_parts));
+    printf("ECV(hash): %zu (%f%%)\n", (size_t)o[3], (double)o[3] / E);
+    printf("  balance: %zu (%f%%)\n", (size_t)o[4], (double)o[4] / (graph.getEdges() / num_parts));
+    printf("ECV(down): %zu (%f%%)\n", (size_t)o[5], (double)o[5] / E);
+    printf("  balance: %zu (%f%%)\n", (size_t)o[6], (double)o[6] / (graph.getEdges() / num_parts));
+    printf("ECV(up)  : %zu (%f%%)\n", (size_t)o[7], (double)o[7] / E);
+    printf("  balance: %zu (%f%%)\n", (size_t)o[8], (double)o[8] / (graph.getEdges() / num_parts));
   }
 
   // writePartitionedGraph (partition.cpp:588-630): edge (X,Y), X<Y, goes to the part of the

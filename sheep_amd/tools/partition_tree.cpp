@@ -16,14 +16,15 @@ using clk = std::chrono::steady_clock;
 static double secs(clk::duration d) { return std::chrono::duration_cast<std::chrono::milliseconds>(d).count() / 1000.0; }
 
 int main(int argc, char* argv[]) {
-  bool verbose = true, do_faqs = false;
+  bool verbose = true, do_faqs = false, gpu_eval = false;
   double balance_factor = 1.03;
   bool vtx_weight = false, pst_weight = false, pre_weight = false;
   const char* graph_filename = "";
   const char* output_filename = "";
   opterr = 0;
   int opt;
-  while ((opt = getopt(argc, argv, "vfb:xdug:o:")) != -1) {
+  // -G (not in the reference): evaluate on the GPU (sheep_evaluate), same output lines
+  while ((opt = getopt(argc, argv, "vfb:xdug:o:G")) != -1) {
     switch (opt) {
       case 'v': verbose = !verbose; break;
       case 'f': do_faqs = !do_faqs; break;
@@ -33,6 +34,7 @@ int main(int argc, char* argv[]) {
       case 'u': pre_weight = true; break;
       case 'g': graph_filename = optarg; break;
       case 'o': output_filename = optarg; break;
+      case 'G': gpu_eval = true; break;
       case '?':
         if (optopt == 'b') printf("Option -%c requires a double.\n", optopt);
         else if (optopt == 'g' || optopt == 'o') printf("Option -%c requires a string.\n", optopt);
@@ -67,7 +69,8 @@ int main(int argc, char* argv[]) {
         Partition p(seq, jnodes, np, balance_factor, vtx_weight, pst_weight, pre_weight);
         if (verbose) printf("Partitioning took: %f seconds\n", secs(clk::now() - ps));
         p.print();
-        p.evaluate(graph, seq);
+        if (gpu_eval) p.evaluate_gpu(graph, seq);
+        else p.evaluate(graph, seq);
       }
     } else {
       std::vector<vid_t> seq = strcmp(argv[optind], "-") == 0 ? fileSequence(graph_filename) : readSequence(argv[optind]);

@@ -94,3 +94,18 @@ def test_graph2tree_partition_output(gpu, oracle, hep_edges, tmp_path):
     parts = oracle.PartTree(p, s).partition(seq, 4)
     n = sum(1 for q in range(4) for _ in open("%s%04d" % (prefix, q)))
     assert n == len(hep_edges)
+
+
+def test_partition_tree_gpu_evaluation_prints_the_same(gpu, tmp_path):
+    """partition_tree -G evaluates on the GPU (sheep_evaluate): every evaluation line equals the
+    host evaluation's, and ECV(down) the published one, for k = 2, 16, 32."""
+    tre = str(tmp_path / "hep.tre")
+    run("graph2tree", HEP, "-o", tre)
+    host = run("partition_tree", "-g", HEP, "-", tre, "2", "16", "32")
+    dev = run("partition_tree", "-G", "-g", HEP, "-", tre, "2", "16", "32")
+    keep = re.compile(r"^(edges cut|Vcom|ECV|  balance)")
+    h = [l for l in host.splitlines() if keep.match(l)]
+    d = [l for l in dev.splitlines() if keep.match(l)]
+    assert len(h) == 3 * 9 and d == h
+    want = {r["k"]: r["ecv_down"] for r in PUB["partitions"]}
+    assert [int(x) for x in re.findall(r"ECV\(down\): (\d+)", dev)] == [want[2], want[16], want[32]]
