@@ -179,16 +179,19 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 // ---- device-level building blocks ---------------------------------------------------------
 
 // Degree: LDS-bucketed histogram for large inputs, global atomics for small ones.
-static void degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
-                       uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s) {
+// Returns true when the bucketed path also counted the rank-gather partition's y digits into
+// the "part_ws" scratch (yhist).
+static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
+                       uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s, bool want_yhist = false) {
   const char* e = getenv("SHEEP_DEGREE");
   bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
   if (!bucketed || n_ids == 0) {
     launch_degree(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, s);
-    return;
+    return false;
   }
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
-  launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s);
+  uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
+  return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist);
 }
 
 // Optional degree information for pst without per-edge atomics (launch_pst_from_degree).
@@ -197,6 +200,7 @@ struct DegInfo {
   const uint32_t* deg = nullptr;    // degrees of THESE records
   const uint32_t* selfc = nullptr;  // self-loop records per vid
   int mode = SHEEP_DEGREE_LLAMA;
+  bool yhist_ready = false;         // degree_dev counted the partition's y digits (part_ws)
 };
 
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
@@ -371,7 +375,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const uint32_t* src = d_uv;
   if (part) {
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
-    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s);
+    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready);
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
   }
@@ -592,11 +596,12 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* selfc = (uint32_t*)c.scratch.get("selfc", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
-  degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s);
+  const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true);
   tm.mark("degree");
   uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
   tm.mark("sequence");
   DegInfo di;
+  di.yhist_ready = yh;
   di.seq = d_seq;
   di.deg = deg;
   di.selfc = selfc;

@@ -48,9 +48,11 @@ void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* 
                             uint32_t* start, uint32_t* end, uint32_t* pst, hipStream_t s);
 // Bucketed LDS degree histogram for large m (same result as launch_degree); selfc nullable.
 size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out);
-void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+// yhist (nullable, 256 words): also counts the y digits of launch_part_gather's first pass
+// (n_rank = n_ids), so that pass needs no counting read; returns true when it did.
+bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
-                            hipStream_t s);
+                            hipStream_t s, uint32_t* yhist = nullptr);
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max,[1]=zeros*/,
                       hipStream_t s);
 // Exclusive scan of n u32 (n < 2^32); tmp needs scan_tmp_words(n) u32.
@@ -77,7 +79,8 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s);
+                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
+                        bool yhist_ready = false);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
                            hipStream_t s);

@@ -269,11 +269,17 @@ static constexpr int DEGB_CHUNK = 32768;  // edges per chunk (<= 65536 endpoints
 static constexpr uint32_t DEGB_NB = 1024;
 static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgroup
 
+// Digit of the first partition pass of the rank gathers (launch_part_gather): 256 id ranges.
+__device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, 255u); }
+
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
-             uint32_t NB, uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t* err) {
+             uint32_t NB, uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t* err,
+             int psh, uint32_t* __restrict__ yhist) {
   __shared__ uint32_t hist[DEGB_NB];
+  __shared__ uint32_t yh[256];  // y digits of the later rank-gather partition (nullable yhist)
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) yh[i] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
   const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
@@ -292,9 +298,13 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
       if (e[u].x >= n_ids || e[u].y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
       atomicAdd(&hist[e[u].x >> SH], 1u);
       if (file_mode || e[u].x != e[u].y) atomicAdd(&hist[e[u].y >> SH], 1u);
+      if (yhist) atomicAdd(&yh[part_digit(e[u].y, psh)], 1u);
     }
   }
   __syncthreads();
+  if (yhist)
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+      if (yh[i]) atomicAdd(&yhist[i], yh[i]);
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x)
     counts[(uint64_t)i * nchunks + blockIdx.x] = hist[i];
 }
@@ -430,18 +440,22 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 }
 
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
-void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t* yhist) {
   int SH;
   uint32_t NB;
   if (!degb_params(n_ids, &SH, &NB)) {
     launch_degree(uv, m, n_ids, file_mode, deg, selfc, err, s);
-    return;
+    return false;
   }
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
-  if (n_ids == 0) return;
-  if (m == 0) { (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s); return; }
+  if (n_ids == 0) return false;
+  if (m == 0) { (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s); return false; }
+  int pbits = 0;
+  for (uint32_t v = n_ids - 1; v; v >>= 1) ++pbits;
+  const int psh = pbits > 8 ? pbits - 8 : 0;  // as launch_part_gather with n_rank = n_ids
+  if (yhist) (void)hipMemsetAsync(yhist, 0, 256 * 4, s);
   uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   uint64_t cw = (uint64_t)NB * nchunks;
   uint32_t* counts = tmp;
@@ -450,7 +464,7 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   uint16_t* ep = (uint16_t*)(((uintptr_t)(stmp + scan_tmp_words(cw)) + 15) & ~(uintptr_t)15);
   uint32_t H = SH > 15 ? 2u : 1u;
   hipLaunchKernelGGL(k_degb_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
-                     n_ids, file_mode, SH, NB, counts, nchunks, err);
+                     n_ids, file_mode, SH, NB, counts, nchunks, err, psh, yhist);
   launch_scan_exclusive(counts, offsets, cw, stmp, s);
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
@@ -458,6 +472,7 @@ void launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                      (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
                      deg);
+  return yhist != nullptr;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -813,7 +828,6 @@ static constexpr int PT_THREADS = 1024;
 static constexpr int PT_ITEMS = 16;
 static constexpr int PT_TILE = PT_THREADS * PT_ITEMS;  // 16384 records, 128 KB LDS stage
 
-__device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, 255u); }
 
 // Global histogram of the y digits (the first partition's run sizes).
 __global__ void __launch_bounds__(PT_THREADS)
@@ -919,7 +933,8 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
 
 // uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: 512 u32 + 256 u64.
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s) {
+                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
+                        bool yhist_ready) {
   if (m == 0) return;
   int bits = 0;
   for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
@@ -927,8 +942,12 @@ void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, ui
   uint32_t* yhist = ws;
   uint32_t* xhist = ws + 256;
   unsigned long long* cursor = (unsigned long long*)(ws + 512);
-  (void)hipMemsetAsync(ws, 0, 512 * 4, s);
-  hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
+  if (yhist_ready) {  // counted by the degree pass (launch_degree_bucketed)
+    (void)hipMemsetAsync(xhist, 0, 256 * 4, s);
+  } else {
+    (void)hipMemsetAsync(ws, 0, 512 * 4, s);
+    hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
+  }
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
   uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
   hipLaunchKernelGGL(k_part<0>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)uv, m,
