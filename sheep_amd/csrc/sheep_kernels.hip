@@ -1355,7 +1355,6 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
   // elimination-tree root.  Membership is tested on the root, not on the label, which the
   // apply of the previous bucket may be rewriting meanwhile.
   const uint32_t RG = (anchor != INV && mapmode <= 1) ? uf_find_ro(uf, anchor) : INV;
-
   const uint32_t G = RG != INV ? label[RG] : INV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
