@@ -83,9 +83,12 @@ def test_sharded_equals_serial(oracle, world):
     scale = 11
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), scale, q), nprocs=world, join=True,
-                       start_method="spawn")
-    seq, parent, pst = q.get(timeout=60)
+    pc = mp.start_processes(_worker, args=(world, _free_port(), scale, q), nprocs=world,
+                            join=False, start_method="spawn")
+    # read before joining: rank 0 cannot exit while its result still sits in the queue's pipe
+    seq, parent, pst = q.get(timeout=120)
+    while not pc.join(timeout=60):
+        pass
     uv = oracle.rmat(scale, 16, 3)
     oseq = oracle.degree_sequence(uv)
     p, s = oracle.build_tree(uv, oseq)
