@@ -96,6 +96,10 @@ def main():
     ap.add_argument("--cpu-scale", type=int, default=22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the tree against the CPU checker")
+    # rehearsal of the N > 1 path on a one-GPU box (every rank on cuda:0, gloo carrying device
+    # tensors: RCCL refuses two ranks on one device); timings are then meaningless
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--same-device", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,10 +107,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from sheep_amd import capi, device
     from sheep_amd.dist import DeviceOps, build_tree_sharded, shard_bounds
@@ -149,7 +158,11 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
-        for name, ms in capi.last_timings():
+        # N > 1: the partial-tree build of this rank (the merge's own phases are "merge_*")
+        tl = capi.last_timings()
+        if world > 1:
+            tl = list(ops.build_timings) + [("merge_" + k, v) for k, v in tl]
+        for name, ms in tl:
             phase.setdefault(name, []).append(ms)
     torch.cuda.synchronize()
     barrier()

@@ -74,7 +74,11 @@ class DeviceOps:
         return self.d.sequence(deg)
 
     def build_tree(self, uv, rmap, seq, n_seq, deg_local, selfc, mode):
-        return self.d.build_tree_deg(uv, rmap, seq, n_seq, deg_local, selfc, mode)
+        out = self.d.build_tree_deg(uv, rmap, seq, n_seq, deg_local, selfc, mode)
+        from . import capi
+
+        self.build_timings = capi.last_timings()  # this rank's partial tree, for the bench
+        return out
 
     def merge_into(self, pa, sa, pb, sb, n):
         self.d.merge_into(pa, sa, pb, sb, n)
