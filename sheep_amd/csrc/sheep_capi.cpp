@@ -227,25 +227,32 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
 // Liu's elimination tree from items sorted by hi down to groups of 2^lo_bit ranks (m items,
 // INVALID his last): the kb bucket loop (or the plain zipper).  parent: n_seq words, INVALID
 // filled; jump: n_seq zeroed words; spare: m free u64 (kept pairs); hcnt: nullable hi counts.
+// Bucket boundaries (rank, first record) of a kb loop, ending with (n_seq, m_valid).
+using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
+
+// kb bucket counts: each bucket costs a fixed ~60-100 us of launches and small kernels, while
+// too few buckets leave the zipper long in-bucket walks (profiles/r01/kb_bucket_sweep.txt).
+static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r) {
+  const char* ek = getenv("SHEEP_KB_BUCKETS");
+  const char* er = getenv("SHEEP_KB_RANKB");
+  const uint32_t K_auto = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, m >> 23));
+  *K_e = ek ? (uint32_t)atoi(ek) : K_auto;
+  *K_r = er ? (uint32_t)atoi(er) : K_auto;
+}
+
 static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, uint64_t m,
                              uint32_t n_seq, int lo_bit, uint32_t* d_parent, uint32_t* jump,
                              uint32_t* hcnt, bool kb, bool stats, unsigned long long* ws,
-                             hipStream_t s, Timer* tm) {
+                             hipStream_t s, Timer* tm, const Buckets* given = nullptr,
+                             const uint32_t* bins = nullptr, uint32_t nb = 0) {
   const char* es = getenv("SHEEP_TREE_STATS");
   if (!kb) {
     const char* ev = getenv("SHEEP_TREE_VARIANT");
     int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
     launch_tree_insert(sorted, m, d_parent, jump, variant, stats, ws, s);
   } else {
-    const char* ek = getenv("SHEEP_KB_BUCKETS");
-    const char* er = getenv("SHEEP_KB_RANKB");
-    // Bucket counts grow with the input: each bucket costs a fixed ~60-100 us of launches and
-    // small kernels, while too few buckets leave the zipper long in-bucket walks.  Measured
-    // (profiles/r01/kb_bucket_sweep.txt): LJ-shape (69M records) is best at 8 + 8, R-MAT-26
-    // (1.07G) and twitter-shape (1.47G) at 64 + 64.
-    const uint32_t K_auto = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, m >> 23));
-    uint32_t K_e = ek ? (uint32_t)atoi(ek) : K_auto;
-    uint32_t K_r = er ? (uint32_t)atoi(er) : K_auto;
+    uint32_t K_e, K_r;
+    kb_counts(m, &K_e, &K_r);
     uint32_t K = K_e + K_r;
     uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
     uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
@@ -261,29 +268,35 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     launch_iota(uf, n_seq, s);
     launch_iota(label, n_seq, s);
     (void)hipMemsetAsync(ws, 0, 64 * 2, s);
-    launch_kb_bounds(sorted, m, K_e, K_r, n_seq, lo_bit, bounds, s);
-    std::vector<unsigned long long> hb(2 * (K + 1));
-    HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    Buckets bk;
+    uint64_t m_valid = 0;
+    if (given) {
+      bk = *given;
+      m_valid = bk.back().second;
+    } else {
+      launch_kb_bounds(sorted, m, K_e, K_r, n_seq, lo_bit, bounds, s);
+      std::vector<unsigned long long> hb(2 * (K + 1));
+      HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      m_valid = hb[2 * K + 1];
+      // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
+      std::vector<std::pair<uint32_t, uint64_t>> cand;
+      for (uint32_t k = 0; k < K; ++k) cand.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
+      std::sort(cand.begin(), cand.end());
+      for (auto& cb : cand)
+        if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
+      if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
+      bk.emplace_back(n_seq, m_valid);
+    }
     if (tm) tm->mark("kb_bounds");
-    uint64_t m_valid = hb[2 * K + 1];
-    // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
-    std::vector<std::pair<uint32_t, uint64_t>> cand;
-    for (uint32_t k = 0; k < K; ++k) cand.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
-    std::sort(cand.begin(), cand.end());
-    std::vector<std::pair<uint32_t, uint64_t>> bk;
-    for (auto& cb : cand)
-      if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
-    if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
-    bk.emplace_back(n_seq, m_valid);
-    const size_t nb = bk.size() - 1;
+    const size_t nbk = bk.size() - 1;
     // The sort's free ping-pong buffer (m items) holds the kept (b, g) pairs of a bucket.
     // Pipelined (default): bucket k+1 is mapped on the side stream while bucket k is applied
     // on s, with kept pairs, marks and counters double-buffered by bucket parity — each needs
     // half of the buffer.  The map of bucket k+1 anchors the giant at the last rank of bucket
     // k-1 (launch_kb_map).
     uint64_t max_e = 0;
-    for (size_t k = 0; k < nb; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
+    for (size_t k = 0; k < nbk; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
     const char* epp = getenv("SHEEP_KB_PIPE");
     bool per_bucket = es && es[0] == '2';
     const bool pipe = (epp ? atoi(epp) != 0 : true) && !per_bucket && 2 * max_e <= m;
@@ -299,7 +312,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       int p = par(k);
       size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
       launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
-                    kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws, st);
+                    kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws,
+                    bins, nb, st);
       if (tm) tm->span_end(sp, st);
     };
     auto apply_k = [&](size_t k, hipStream_t st) {
@@ -316,8 +330,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
       map_k(0, s2);
       HIP_CHECK(hipEventRecord(ev_map[0], s2));
-      for (size_t k = 0; k < nb; ++k) {
-        if (k + 1 < nb) {  // map k+1 reuses the buffers of bucket k-1: wait for its apply
+      for (size_t k = 0; k < nbk; ++k) {
+        if (k + 1 < nbk) {  // map k+1 reuses the buffers of bucket k-1: wait for its apply
           if (k >= 1) HIP_CHECK(hipStreamWaitEvent(s2, ev_apply[(k + 1) & 1], 0));
           map_k(k + 1, s2);
           HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
@@ -327,7 +341,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
         HIP_CHECK(hipEventRecord(ev_apply[k & 1], s));
       }
     } else {
-      for (size_t k = 0; k < nb; ++k) {
+      for (size_t k = 0; k < nbk; ++k) {
         if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
         map_k(k, s);
         apply_k(k, s);
@@ -341,6 +355,73 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       }
     }
   }
+}
+
+// ---- hi bins (the one-pass grouping of the edge items, see sheep_kernels.hip) -------------
+// Bin bounds from the 256-rank chunk degree sums: the records with hi in chunk c are estimated
+// as dsum(c) * (D_c + dsum(c)/2) / total, D_c the degree mass of the chunks below.  A bin
+// closes at 1/320 of the estimated records, or when 32K ranks wide (the kb map's LDS window)
+// unless it holds almost nothing; at most 511 bins, then the INVALID bin (bound n_seq).
+static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32_t n_seq) {
+  const size_t nch = dsum.size();
+  std::vector<double> w(nch);
+  double tot = 0, D = 0, W = 0;
+  for (uint64_t d : dsum) tot += (double)d;
+  for (size_t c = 0; c < nch; ++c) {
+    w[c] = tot > 0 ? (double)dsum[c] * (D + 0.5 * (double)dsum[c]) / tot : 0.0;
+    D += (double)dsum[c];
+    W += w[c];
+  }
+  double wmax = W / 320, wide = W / 50000;
+  std::vector<uint32_t> b;
+  for (int attempt = 0; attempt < 32; ++attempt) {
+    b.assign(1, 0u);
+    double acc = 0;
+    for (size_t c = 0; c + 1 < nch; ++c) {
+      acc += w[c];
+      const uint64_t end = (uint64_t)(c + 1) * 256, width = end - b.back();
+      if (acc >= wmax || (width >= 32768 && acc >= wide)) {
+        b.push_back((uint32_t)end);
+        acc = 0;
+      }
+    }
+    if (b.size() + 1 <= 512) break;
+    wide *= 2;
+    wmax *= 1.25;
+  }
+  b.push_back(n_seq);
+  return b;
+}
+
+// Buckets as unions of bins: K_e cuts at edge quantiles (exact bin counts) and K_r at rank
+// quantiles, each snapped to a bin bound.  bin_start: nb + 1 record offsets.
+static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
+                                 const std::vector<unsigned long long>& bin_start, uint64_t m,
+                                 uint32_t n_seq) {
+  const uint32_t nb = (uint32_t)bounds.size();
+  const uint64_t m_valid = bin_start[nb - 1];
+  uint32_t K_e, K_r;
+  kb_counts(m, &K_e, &K_r);
+  std::vector<uint32_t> cuts;
+  for (uint32_t k = 1; k < K_e; ++k) {
+    const uint64_t target = m_valid * k / K_e;
+    uint32_t i = (uint32_t)(std::lower_bound(bin_start.begin(), bin_start.begin() + (nb - 1),
+                                             (unsigned long long)target) - bin_start.begin());
+    if (i > 0 && i < nb - 1) cuts.push_back(i);
+  }
+  for (uint32_t j = 1; j < K_r; ++j) {
+    const uint32_t r = (uint32_t)((uint64_t)n_seq * j / K_r);
+    uint32_t i = (uint32_t)(std::upper_bound(bounds.begin(), bounds.begin() + (nb - 1), r) -
+                            bounds.begin()) - 1;
+    if (i > 0 && i < nb - 1) cuts.push_back(i);
+  }
+  std::sort(cuts.begin(), cuts.end());
+  cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  Buckets bk;
+  bk.emplace_back(0u, 0ull);
+  for (uint32_t i : cuts) bk.emplace_back(bounds[i], (uint64_t)bin_start[i]);
+  bk.emplace_back(n_seq, m_valid);
+  return bk;
 }
 
 static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
@@ -379,11 +460,44 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
   }
-  launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
-                         lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
-  if (tm) tm->mark("edge_pass");
-  const uint64_t* sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
-  uint64_t* spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
+  // Hi bins (one scatter pass) when the degrees are at hand; else the two-pass radix sort.
+  const char* esort = getenv("SHEEP_SORT");
+  const bool use_bins = kb && pst_count && m >= (1ull << 20) && n_seq > 256 &&
+                        !(esort && strcmp(esort, "radix") == 0);
+  const uint64_t* sorted;
+  uint64_t* spare;
+  Buckets given;
+  const uint32_t* dbins = nullptr;
+  uint32_t nbins = 0;
+  if (use_bins) {
+    const size_t nch = ((size_t)n_seq + 255) / 256;
+    uint64_t* cds = (uint64_t*)c.scratch.get("chunk_deg", nch * 8);
+    launch_chunk_degsum(di->seq, di->deg, n_seq, cds, s);
+    std::vector<uint64_t> hd(nch);
+    HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<uint32_t> bounds = make_bins(hd, n_seq);
+    nbins = (uint32_t)bounds.size();
+    uint32_t* db = (uint32_t*)c.scratch.get("hi_bins", 512 * 4);
+    HIP_CHECK(hipMemcpyAsync(db, bounds.data(), nbins * 4, hipMemcpyHostToDevice, s));
+    dbins = db;
+    launch_edge_pass_bins(src, m, d_rank, n_rank, items, c.d_err, db, nbins, tmp, s, part);
+    if (tm) tm->mark("edge_pass");
+    unsigned long long* dstart = (unsigned long long*)c.scratch.get("bin_start", 513 * 8);
+    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, s);
+    std::vector<unsigned long long> hs(nbins + 1);
+    HIP_CHECK(hipMemcpyAsync(hs.data(), dstart, (nbins + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    given = buckets_from_bins(bounds, hs, m, n_seq);
+    sorted = items_b;
+    spare = items;
+  } else {
+    launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
+                           lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
+    if (tm) tm->mark("edge_pass");
+    sorted = radix_sort_u64(items, items_b, items, m, lo_bit, top + 1, tmp, s, true);
+    spare = (sorted == items) ? items_b : items;  // free ping-pong buffer
+  }
   if (tm) tm->mark("bucket_sort");
   uint32_t* hcnt = nullptr;
   if (pst_count) {
@@ -391,7 +505,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_fill(hcnt, 0, n_seq, s);
   }
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
-  tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, kb, stats, ws, s, tm);
+  tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, kb, stats, ws, s, tm,
+                   use_bins ? &given : nullptr, dbins, nbins);
   if (tm) tm->mark("tree_insert");
   if (pst_count) {
     launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s);

@@ -76,6 +76,16 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                             uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
                             uint32_t* tmp, hipStream_t s, bool pre = false);
+// Hi bins (one-pass grouping, see sheep_kernels.hip): chunk degree sums (256 ranks per chunk),
+// the edge pass counting bins (no pst; nb <= 512 bounds, bounds[0] = 0, bounds[nb-1] = n_seq
+// so that INVALID his fall in the last bin), and the scatter by bin (bin_start: nb+1 u64).
+void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_seq, uint64_t* out,
+                         hipStream_t s);
+void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                           uint64_t* items, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                           uint32_t* tmp, hipStream_t s, bool pre);
+void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
+                  uint32_t* tmp, unsigned long long* bin_start, hipStream_t s);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
@@ -96,7 +106,8 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift,
                    uint32_t* cnt /* nullable: hi run lengths */, bool stats,
-                   unsigned long long* st, hipStream_t s);
+                   unsigned long long* st, const uint32_t* bins /* nullable: hi bins */,
+                   uint32_t nb, hipStream_t s);
 // refresh: re-resolve the kept starts against the current union-find first (pipelined loop).
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,

@@ -486,6 +486,17 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
 // per-wave offsets, the tile is staged in LDS in digit order, and written so that
 // consecutive lanes store consecutive addresses of one digit run.
 // ---------------------------------------------------------------------------------------
+// bin of hi: the largest i with bounds[i] <= hi (bounds[0] = 0; INVALID his: the last bin)
+__device__ __forceinline__ uint32_t bin_of(const uint32_t* bounds, uint32_t nb, uint32_t hi) {
+  uint32_t lo = 0, n = nb;
+  while (n > 1) {
+    uint32_t half = n >> 1;
+    if (bounds[lo + half] <= hi) lo += half;
+    n -= half;
+  }
+  return lo;
+}
+
 static constexpr int RS_THREADS = 1024;
 static constexpr int RS_ITEMS = 8;
 static constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
@@ -533,14 +544,21 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
     counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
-template <int DB>
+template <int DB, bool BINS = false>
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n, int shift,
-                const uint32_t* __restrict__ offsets, uint32_t ntiles) {
+                const uint32_t* __restrict__ offsets, uint32_t ntiles,
+                const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint64_t stage[RS_TILE];
   __shared__ uint32_t whist[RS_WAVES][NBIN];
   __shared__ uint32_t tstart[NBIN], goff[NBIN], wsum[RS_WAVES];
+  __shared__ uint32_t sb[BINS ? NBIN : 1];
+  __shared__ uint16_t stage_d[BINS ? RS_TILE : 1];  // bins: the digit of each staged item
+  auto digit = [&](uint64_t it) -> uint32_t {
+    const uint32_t hi = (uint32_t)(it >> 32);
+    return BINS ? bin_of(sb, nb, hi) : (uint32_t)(it >> (32 + shift)) & (NBIN - 1);
+  };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
   const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : RS_TILE);
@@ -548,6 +566,11 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (uint32_t i = t; i < NBIN; i += RS_THREADS) goff[i] = offsets[(uint64_t)i * ntiles + blockIdx.x];
   for (uint32_t i = lane; i < NBIN; i += 64) whist[w][i] = 0;
+  if (BINS) {
+    for (uint32_t i = t; i < nb; i += RS_THREADS) sb[i] = bins[i];
+    __syncthreads();
+  }
+  uint32_t dg[RS_ITEMS];
   uint64_t item[RS_ITEMS];
   uint32_t rk[RS_ITEMS];
 #pragma unroll
@@ -559,7 +582,8 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     bool valid = wbase + (uint32_t)k * 64 < tile_n;
-    uint32_t d = (uint32_t)(item[k] >> (32 + shift)) & (NBIN - 1);
+    uint32_t d = digit(item[k]);
+    dg[k] = d;
     uint64_t match = digit_match<DB>(d, valid);
     uint32_t before = (uint32_t)__popcll(match & lt);
     uint32_t prev = whist[w][d];
@@ -586,16 +610,39 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     if (wbase + (uint32_t)k * 64 < tile_n) {
-      uint32_t d = (uint32_t)(item[k] >> (32 + shift)) & (NBIN - 1);
+      uint32_t d = dg[k];
       stage[tstart[d] + whist[w][d] + rk[k]] = item[k];
+      if (BINS) stage_d[tstart[d] + whist[w][d] + rk[k]] = (uint16_t)d;
     }
   }
   __syncthreads();
   for (uint32_t j = t; j < tile_n; j += RS_THREADS) {
     uint64_t it = stage[j];
-    uint32_t d = (uint32_t)(it >> (32 + shift)) & (NBIN - 1);
+    uint32_t d = BINS ? (uint32_t)stage_d[j] : digit(it);
     out[(uint64_t)goff[d] + (j - tstart[d])] = it;
   }
+}
+
+// Records grouped by hi bin in one pass (the hi-bin alternative to radix_sort_u64): the
+// tile histograms were counted by the edge pass (launch_edge_pass_bins).  bin_start (device,
+// nb + 1 u64) receives where each bin starts in `out`, and the total.
+__global__ void k_bin_starts(const uint32_t* __restrict__ offsets, uint32_t ntiles, uint32_t nb,
+                             uint64_t n, unsigned long long* __restrict__ bin_start) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= nb; d += gridDim.x * blockDim.x)
+    bin_start[d] = d < nb ? offsets[(uint64_t)d * ntiles] : n;
+}
+
+void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
+                  uint32_t* tmp, unsigned long long* bin_start, hipStream_t s) {
+  uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
+  uint32_t* counts = tmp;
+  uint32_t* stmp = tmp + 512 * nt;
+  launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
+  hipLaunchKernelGGL(k_bin_starts, dim3(3), dim3(BLOCK), 0, s, (const uint32_t*)counts, (uint32_t)nt,
+                     nb, n, bin_start);
+  if (n)
+    hipLaunchKernelGGL((k_rsort_scatter<9, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in, out,
+                       n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb);
 }
 
 size_t rsort_tmp_words(uint64_t n) {
@@ -631,14 +678,14 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
                              shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt);
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
       } else {
         if (count)
           hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
                              shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt);
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
       }
     }
     shift += width;
@@ -731,6 +778,39 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
                      n_rank, pst, items, err);
 }
 
+// ---------------------------------------------------------------------------------------
+// Hi bins: one radix-style pass instead of the two 9-bit passes.  The kb loop needs the
+// records grouped by hi only down to 256-rank groups, and only where they are dense; the bins
+// are runs of 256-rank chunks cut from an estimate of the records per hi rank taken from the
+// degrees alone (a vertex of degree d at rank r is the hi end of about d * D(r) / 2m records,
+// D(r) the degree mass below r), so they exist before the edge pass computes a single hi.
+// The estimate only shapes the work; any bins give the same tree.
+// ---------------------------------------------------------------------------------------
+// out[c] = sum of deg[seq[r]] over r in [256 c, 256 c + 256) (one wave per chunk).
+__global__ void k_chunk_degsum(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ deg,
+                               uint32_t n_seq, uint64_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nch = (n_seq + 255) / 256;
+  for (uint32_t ch = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; ch < nch;
+       ch += (gridDim.x * blockDim.x) >> 6) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t r = ch * 256 + k * 64 + lane;
+      if (r < n_seq) sum += deg[seq[r]];
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o);
+    if (lane == 0) out[ch] = sum;
+  }
+}
+
+void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_seq, uint64_t* out,
+                         hipStream_t s) {
+  if (n_seq) hipLaunchKernelGGL(k_chunk_degsum, dim3(grid_for((uint64_t)(n_seq + 255) / 256 * 64)),
+                                dim3(BLOCK), 0, s, seq, deg, n_seq, out);
+}
+
+
 // The edge pass fused with the first radix pass's tile histograms (digit = bits
 // [shift, shift + DB) of hi): one block per RS_TILE records, wave-striped like
 // k_rsort_count; each thread loads its 8 records and issues their rank gathers before using
@@ -740,15 +820,19 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
 constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
 
-template <int DB, bool PRE>
+template <int DB, bool PRE, bool BINS = false>
 __global__ void __launch_bounds__(RS_THREADS)
 k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
                   uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
-                  uint32_t* err, int shift, uint32_t* __restrict__ counts, uint32_t ntiles) {
+                  uint32_t* err, int shift, uint32_t* __restrict__ counts, uint32_t ntiles,
+                  const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint32_t hist[NBIN];
+  __shared__ uint32_t sb[BINS ? NBIN : 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (uint32_t i = t; i < NBIN; i += RS_THREADS) hist[i] = 0;
+  if (BINS)
+    for (uint32_t i = t; i < nb; i += RS_THREADS) sb[i] = bins[i];
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (64 * RS_ITEMS) + lane;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint2 e[RS_ITEMS];
@@ -789,7 +873,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
       }
     }
     if (valid) items[idx] = ((uint64_t)hi << 32) | lo;
-    uint32_t d = (hi >> shift) & (NBIN - 1);
+    uint32_t d = BINS ? bin_of(sb, nb, hi) : (hi >> shift) & (NBIN - 1);
     uint64_t match = digit_match<DB>(d, valid);
     if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
   }
@@ -801,6 +885,17 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
 // Edge pass whose output feeds radix_sort_u64(..., bit_lo = shift, counted0 = true): tmp is
 // that sort's tmp (rsort_tmp_words(m)); DB = rsort_first_width of the sorted bit range.
 // pre: uv holds k_part's (x, ry) records.
+void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                           uint64_t* items, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                           uint32_t* tmp, hipStream_t s, bool pre) {
+  if (m == 0) return;
+  uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
+  if (nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
+  auto k = pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>;
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
+                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb);
+}
+
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                             uint32_t* pst, uint64_t* items, uint32_t* err, int shift, int DB,
                             uint32_t* tmp, hipStream_t s, bool pre) {
@@ -809,7 +904,7 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
   auto k = DB > 8 ? (pre ? k_edge_pass_tiles<9, true> : k_edge_pass_tiles<9, false>)
                   : (pre ? k_edge_pass_tiles<8, true> : k_edge_pass_tiles<8, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
-                     pst, items, err, shift, tmp, (uint32_t)nt);
+                     pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1345,7 +1440,7 @@ __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
          int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode,
-         uint32_t anchor) {
+         uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -1363,10 +1458,19 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
        c0 += (uint64_t)gridDim.x * KM_CHUNK) {
     const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, e_end);
     // every record of the chunk has b >= the first record's group start
-    const uint32_t bbase = (((uint32_t)(items[c0] >> 32) >> gshift) << gshift) & ~31u;
+    // the chunk's records lie in [group (or bin) of its first record, that of its last)
+    const uint32_t h0 = (uint32_t)(items[c0] >> 32);
     const uint32_t blast = (uint32_t)(items[c1 - 1] >> 32);
-    const uint32_t gend = (uint32_t)min((((uint64_t)(blast >> gshift)) + 1) << gshift,
-                                        (uint64_t)bbase + KM_WIN);
+    uint32_t bbase, gend;
+    if (bins) {
+      bbase = bins[bin_of(bins, nb, h0)] & ~31u;
+      gend = (uint32_t)min((uint64_t)bins[min(bin_of(bins, nb, blast) + 1, nb - 1)],
+                           (uint64_t)bbase + KM_WIN);
+      if (gend <= bbase) gend = bbase + 1;
+    } else {
+      bbase = ((h0 >> gshift) << gshift) & ~31u;
+      gend = (uint32_t)min((((uint64_t)(blast >> gshift)) + 1) << gshift, (uint64_t)bbase + KM_WIN);
+    }
     const uint32_t span = gend - bbase;  // ranks of the window that can hold records
     for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) wbits[i] = 0;
     if (cnt)
@@ -1635,7 +1739,7 @@ static int kb_mapmode() {
 void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
-                   unsigned long long* st, hipStream_t s) {
+                   unsigned long long* st, const uint32_t* bins, uint32_t nb, hipStream_t s) {
   const int mapmode = kb_mapmode();
   if (mapmode > 1) anchor = INV;
   if (e_end <= e_begin) return;
@@ -1643,7 +1747,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
-                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor);
+                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor, bins, nb);
 }
 
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,

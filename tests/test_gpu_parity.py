@@ -291,6 +291,7 @@ KB_KNOBS = [
     {"SHEEP_TREE_ALGO": "zip"},                            # plain zipper, no buckets
     {"SHEEP_KB_PIPE": "0"},                                # one stream, map of bucket k after apply of k-1
     {"SHEEP_KB_REFRESH": "0"},                             # pipelined, stale kept starts zipped as they are
+    {"SHEEP_SORT": "radix"},                               # two 9-bit radix passes instead of hi bins
     {"SHEEP_KB_PIPE": "1", "SHEEP_KB_BUCKETS": "512", "SHEEP_KB_RANKB": "512"},  # many narrow buckets
 ]
 
