@@ -481,10 +481,11 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     uint32_t* db = (uint32_t*)c.scratch.get("hi_bins", 512 * 4);
     HIP_CHECK(hipMemcpyAsync(db, bounds.data(), nbins * 4, hipMemcpyHostToDevice, s));
     dbins = db;
-    launch_edge_pass_bins(src, m, d_rank, n_rank, items, c.d_err, db, nbins, tmp, s, part);
+    uint16_t* digits = (uint16_t*)c.scratch.get("item_bins", m * 2);
+    launch_edge_pass_bins(src, m, d_rank, n_rank, items, c.d_err, db, nbins, tmp, digits, s, part);
     if (tm) tm->mark("edge_pass");
     unsigned long long* dstart = (unsigned long long*)c.scratch.get("bin_start", 513 * 8);
-    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, s);
+    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, digits, s);
     std::vector<unsigned long long> hs(nbins + 1);
     HIP_CHECK(hipMemcpyAsync(hs.data(), dstart, (nbins + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));

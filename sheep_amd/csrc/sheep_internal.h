@@ -81,11 +81,13 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
 // so that INVALID his fall in the last bin), and the scatter by bin (bin_start: nb+1 u64).
 void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_seq, uint64_t* out,
                          hipStream_t s);
+// digits: m u16 scratch (each item's bin, written by the edge pass, read by the scatter)
 void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                            uint64_t* items, uint32_t* err, const uint32_t* bins, uint32_t nb,
-                           uint32_t* tmp, hipStream_t s, bool pre);
+                           uint32_t* tmp, uint16_t* digits, hipStream_t s, bool pre);
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
-                  uint32_t* tmp, unsigned long long* bin_start, hipStream_t s);
+                  uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
+                  hipStream_t s);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,

@@ -548,7 +548,8 @@ template <int DB, bool BINS = false>
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n, int shift,
                 const uint32_t* __restrict__ offsets, uint32_t ntiles,
-                const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0) {
+                const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0,
+                const uint16_t* __restrict__ digits = nullptr) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint64_t stage[RS_TILE];
   __shared__ uint32_t whist[RS_WAVES][NBIN];
@@ -577,12 +578,13 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   for (int k = 0; k < RS_ITEMS; ++k) {
     uint32_t li = wbase + (uint32_t)k * 64;
     item[k] = li < tile_n ? in[tbase + li] : 0ull;
+    if (BINS) dg[k] = li < tile_n ? digits[tbase + li] : 0u;
   }
   // stable rank inside the wave: rounds in item order, lanes in item order within a round
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     bool valid = wbase + (uint32_t)k * 64 < tile_n;
-    uint32_t d = digit(item[k]);
+    uint32_t d = BINS ? dg[k] : digit(item[k]);
     dg[k] = d;
     uint64_t match = digit_match<DB>(d, valid);
     uint32_t before = (uint32_t)__popcll(match & lt);
@@ -633,7 +635,8 @@ __global__ void k_bin_starts(const uint32_t* __restrict__ offsets, uint32_t ntil
 }
 
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
-                  uint32_t* tmp, unsigned long long* bin_start, hipStream_t s) {
+                  uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
+                  hipStream_t s) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   uint32_t* stmp = tmp + 512 * nt;
@@ -642,7 +645,7 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
                      nb, n, bin_start);
   if (n)
     hipLaunchKernelGGL((k_rsort_scatter<9, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in, out,
-                       n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb);
+                       n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
 }
 
 size_t rsort_tmp_words(uint64_t n) {
@@ -678,14 +681,16 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
                              shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
+                           (const uint16_t*)nullptr);
       } else {
         if (count)
           hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
                              shift, counts, (uint32_t)nt);
         launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
         hipLaunchKernelGGL(k_rsort_scatter<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
+                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
+                           (const uint16_t*)nullptr);
       }
     }
     shift += width;
@@ -825,7 +830,8 @@ __global__ void __launch_bounds__(RS_THREADS)
 k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
                   uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
                   uint32_t* err, int shift, uint32_t* __restrict__ counts, uint32_t ntiles,
-                  const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0) {
+                  const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0,
+                  uint16_t* __restrict__ digits = nullptr) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint32_t hist[NBIN];
   __shared__ uint32_t sb[BINS ? NBIN : 1];
@@ -874,6 +880,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
     }
     if (valid) items[idx] = ((uint64_t)hi << 32) | lo;
     uint32_t d = BINS ? bin_of(sb, nb, hi) : (hi >> shift) & (NBIN - 1);
+    if (BINS && valid) digits[idx] = (uint16_t)d;  // the scatter pass reads it back
     uint64_t match = digit_match<DB>(d, valid);
     if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
   }
@@ -887,13 +894,13 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
 // pre: uv holds k_part's (x, ry) records.
 void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                            uint64_t* items, uint32_t* err, const uint32_t* bins, uint32_t nb,
-                           uint32_t* tmp, hipStream_t s, bool pre) {
+                           uint32_t* tmp, uint16_t* digits, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
   if (nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
   auto k = pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>;
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
-                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb);
+                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits);
 }
 
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
@@ -904,7 +911,8 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
   auto k = DB > 8 ? (pre ? k_edge_pass_tiles<9, true> : k_edge_pass_tiles<9, false>)
                   : (pre ? k_edge_pass_tiles<8, true> : k_edge_pass_tiles<8, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
-                     pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u);
+                     pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
+                     (uint16_t*)nullptr);
 }
 
 // ---------------------------------------------------------------------------------------
