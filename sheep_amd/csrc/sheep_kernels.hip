@@ -416,6 +416,75 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
     if (g0 + i < n_ids) deg[g0 + i] = cnt[i];
 }
 
+// Buckets of 65536 ids (n_ids > 2^25): one workgroup per bucket reads the bucket's run ONCE
+// (k_degb_hist needs two workgroups there, each reading the whole run for its half).  The
+// 65536 counters are u16 halves of 32768 LDS words; the run is counted in segments of at most
+// 65535 entries, so no half can carry into its neighbour, and after each segment every thread
+// folds its 64 ids into u32 registers.
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
+              const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, uint32_t n_ids,
+              uint32_t* __restrict__ deg) {
+  __shared__ uint32_t pk[32768];
+  const uint32_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint64_t s0 = offsets[(uint64_t)b * nchunks];
+  const uint64_t last = (uint64_t)NB * nchunks - 1;
+  const uint64_t s1 = (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                   : (uint64_t)offsets[last] + counts[last];
+  uint32_t acc[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) acc[k] = 0;
+  constexpr int V = 4;
+  for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
+    const uint64_t g1 = min(g0 + 65535, s1);
+    for (uint32_t i = threadIdx.x; i < 32768; i += DEGB_THREADS) pk[i] = 0;
+    __syncthreads();
+    for (uint64_t i0 = g0 & ~7ull; i0 < g1; i0 += 8 * V * DEGB_THREADS) {
+      uint4 q[V];
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
+        q[u] = i < g1 ? *(const uint4*)(ep + i) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
+        uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint64_t ik = i + k;
+          uint32_t v = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+          bool done = !(ik >= g0 && ik < g1);
+          // one round of leader matching folds a hub's repeated id into one LDS add
+          uint64_t act = __ballot(!done);
+          if (act) {
+            int leader = __ffsll((unsigned long long)act) - 1;
+            uint32_t lv = __builtin_amdgcn_readlane(v, leader);
+            uint64_t same = __ballot(!done && v == lv);
+            if (lane == leader) atomicAdd(&pk[lv >> 1], (uint32_t)__popcll(same) << (16 * (lv & 1)));
+            if ((same >> lane) & 1) done = true;
+            if (!done) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      const uint32_t id = (uint32_t)k * DEGB_THREADS + threadIdx.x;
+      acc[k] += (pk[id >> 1] >> (16 * (id & 1))) & 0xFFFFu;
+    }
+    __syncthreads();
+  }
+  const uint64_t base = (uint64_t)b << 16;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const uint64_t id = base + (uint64_t)k * DEGB_THREADS + threadIdx.x;
+    if (id < n_ids) deg[id] = acc[k];
+  }
+}
+
 // SH: local-id bits, NB buckets; false when n_ids is beyond the bucketed path (> 2^26).
 static bool degb_params(uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
   int bits = 0;
@@ -469,9 +538,14 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
                      nchunks, ep, selfc);
-  hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
-                     (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
-                     deg);
+  const char* eh = getenv("SHEEP_DEGB_HIST");
+  if (H > 1 && !(eh && atoi(eh) == 0))
+    hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg);
+  else
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
+                       deg);
   return yhist != nullptr;
 }
 

@@ -370,3 +370,32 @@ def test_evaluate_rejects_missing_part(api):
     with pytest.raises(capi.SheepError) as e:
         device.evaluate(uv, parts, rank, n_parts=1)
     assert e.value.code == -34  # -ERANGE
+
+
+@pytest.mark.parametrize("hist", ["1", "0"])
+def test_degree_64k_id_buckets(oracle, api, monkeypatch, hist):
+    """Id spaces above 2^25 use buckets of 65536 ids: the one-read histogram with u16 LDS
+    counters in segments of <= 65535 entries (hist=1) and the two-half one (hist=0) give the
+    checker's degrees — with a hub repeated more than 65535 times in one bucket, so counts
+    cross the u16 range across segments."""
+    import torch
+    from sheep_amd import capi, device
+
+    monkeypatch.setenv("SHEEP_DEGB_HIST", hist)
+    monkeypatch.setenv("SHEEP_DEGREE", "bucketed")
+    rng = np.random.default_rng(7)
+    n_ids = (1 << 26) + 5
+    m = 1 << 20
+    uv = rng.integers(0, n_ids, size=(m, 2)).astype(np.uint32)
+    dense = rng.random(m) < 0.25  # a quarter of the records inside bucket 3
+    uv[dense] = (3 << 16) + rng.integers(0, 4000, size=(int(dense.sum()), 2)).astype(np.uint32)
+    hub = rng.random(m) < 0.12  # ~126K occurrences of one id of bucket 3
+    uv[hub, 0] = (3 << 16) + 17
+    loops = rng.random(m) < 0.03
+    uv[loops, 1] = uv[loops, 0]
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    for mode in (capi.DEGREE_LLAMA, capi.DEGREE_FILE):
+        got = device.degree(uv_d, n_ids, mode).cpu().numpy().view(np.uint32)
+        want = oracle.degree(uv, mode, n_ids)
+        assert np.array_equal(got, want)
+        assert got[(3 << 16) + 17] > 65535
