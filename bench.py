@@ -100,6 +100,10 @@ def main():
     # tensors: RCCL refuses two ranks on one device); timings are then meaningless
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--same-device", action="store_true")
+    # N > 1: lockstep (one kb loop walked by all ranks, kept pairs all-gathered per bucket) or
+    # merge (per-rank partial trees, gathered and merged on rank 0)
+    ap.add_argument("--dist", default=os.environ.get("SHEEP_DIST", "lockstep"),
+                    choices=["lockstep", "merge"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,7 +122,7 @@ def main():
             dist.init_process_group("gloo")
 
     from sheep_amd import capi, device
-    from sheep_amd.dist import DeviceOps, build_tree_sharded, shard_bounds
+    from sheep_amd.dist import DeviceOps, build_tree_lockstep, build_tree_sharded, shard_bounds
 
     device.init(local)
     scale, ef, seed = args.scale, args.edgefactor, args.seed
@@ -149,6 +153,8 @@ def main():
     def step():
         if world == 1:
             return device.graph2tree(uv, n_ids)
+        if args.dist == "lockstep":
+            return build_tree_lockstep(uv, n_ids, ops)
         return build_tree_sharded(uv, n_ids, ops)
 
     for _ in range(args.warmup):
@@ -160,7 +166,7 @@ def main():
         out = step()
         # N > 1: the partial-tree build of this rank (the merge's own phases are "merge_*")
         tl = capi.last_timings()
-        if world > 1:
+        if world > 1 and args.dist == "merge":
             tl = list(ops.build_timings) + [("merge_" + k, v) for k, v in tl]
         for name, ms in tl:
             phase.setdefault(name, []).append(ms)
@@ -213,7 +219,8 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "u32",
             "data": data,
             "config": dict(wl, records=m, n_ids=n_ids, n_seq=n_seq,
-                           parallelism="edge-shard x%d" % world if world > 1 else "single"),
+                           parallelism=("edge-shard x%d (%s)" % (world, args.dist)
+                                        if world > 1 else "single")),
             "path_roofline": {"bytes": path_bytes,
                               "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK)},
             "roofline": roof,

@@ -123,6 +123,46 @@ int sheep_merge_trees_dev(uint32_t* d_parent_a, uint32_t* d_pst_a, const uint32_
 int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_t n,
                             uint32_t* d_parent_out, void* stream);
 
+/* ---- lockstep multi-GPU tree build (graph2tree -i -r, graph2tree.cpp:134-200) -----------
+ * The elimination tree of the union of P edge shards, one shard per rank, without partial
+ * trees: every rank keeps the SAME union-find and forest and walks the same rank buckets; per
+ * bucket it maps only its own records (sheep_ls_map), the caller all-gathers the packed
+ * contributions (sheep_ls_pack) of all ranks over RCCL, and every rank applies the union
+ * (sheep_ls_apply).  Replaces the per-rank JTree + mpi_merge (jnode.cpp:213-250) reduce; the
+ * result equals the serial tree (the etree is unique).  Call sequence per rank:
+ *   sheep_ls_begin   this shard's records -> hi-binned items; bin bounds come from the GLOBAL
+ *                    degrees d_deg (after the degree all-reduce), so they agree on every rank;
+ *                    bin_counts_out (host, >= 512 words) receives this shard's records per bin
+ *                    and *n_bins_out their number.  Synchronises.  *handle_out owns the state.
+ *   sheep_ls_plan    with the bin counts summed over ranks: *n_buckets_out buckets and the
+ *                    mark slots S of a contribution (host only).
+ *   per bucket k:    sheep_ls_map(k, d_send) maps into d_send (>= S + m u64); this rank's
+ *                    kept-pair count goes to d_count (device int64, nullable; enqueue only)
+ *                    and/or *n_kept_out (host, nullable; synchronises); cap = max over ranks;
+ *                    sheep_ls_pack(k, d_send, cap) lays out S + cap u64 (d_send must hold
+ *                    them: cap may exceed this shard's m);
+ *                    [all-gather of d_send[0, S + cap) from every rank into d_recv];
+ *                    sheep_ls_apply(k, d_recv, P, cap).
+ *   sheep_ls_finish  d_parent (n_seq, identical on every rank) and d_pst (n_seq) of THIS
+ *                    shard's records from its own degrees d_deg / d_selfc (sum over ranks =
+ *                    the tree's pst_weight).  Synchronises.
+ *   sheep_ls_free    releases the state. */
+int sheep_ls_begin(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_rank,
+                   const uint32_t* d_seq, uint32_t n_seq, const uint32_t* d_deg,
+                   uint64_t* bin_counts_out, uint32_t* n_bins_out, void** handle_out,
+                   void* stream);
+int sheep_ls_plan(void* handle, const uint64_t* global_bin_counts, uint32_t* n_buckets_out,
+                  uint32_t* mark_slots_out);
+int sheep_ls_map(void* handle, uint32_t k, uint64_t* d_send, int64_t* d_count,
+                 uint32_t* n_kept_out, void* stream);
+int sheep_ls_pack(void* handle, uint32_t k, uint64_t* d_send, uint32_t cap, void* stream);
+int sheep_ls_apply(void* handle, uint32_t k, const uint64_t* d_recv, uint32_t n_ranks,
+                   uint32_t cap, void* stream);
+int sheep_ls_finish(void* handle, const uint32_t* d_seq, const uint32_t* d_deg,
+                    const uint32_t* d_selfc, int degree_mode, uint32_t* d_parent, uint32_t* d_pst,
+                    void* stream);
+int sheep_ls_free(void* handle);
+
 /* Partition quality of a k-way vertex partition (Partition::evaluate(graph) and
  * evaluate(graph, seq), partition.cpp:428-521) over the m edge records in HBM, counted on
  * LLAMA's undirected adjacency as the reference does.  d_parts: n_ids int16 parts (every id

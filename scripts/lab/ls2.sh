@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_lockstep_gpu.py tests/test_dist_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ls_test.log 2>&1 && echo "ls tests ok" &&
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --same-device --check --scale 20 --steps 2 --warmup 1 > gpurun_out/ls_bench2.log 2>&1 && echo "bench2 ok" &&
+for K in 16 32 48; do SHEEP_KB_BUCKETS=$K SHEEP_KB_RANKB=$K timeout -k 10 300 python scripts/lockstep_sim.py --scale 26 --P 8 --reps 1 >> gpurun_out/ls_sweep.log 2>&1 || exit 1; echo "K=$K ok"; done

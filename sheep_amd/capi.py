@@ -75,6 +75,14 @@ def lib():
         "sheep_powerlaw_dev": [u32p, c.c_uint32, c.c_double, c.c_double, c.c_uint64, c.c_uint64,
                                c.c_uint64, vp],
         "sheep_last_timings": [c.c_void_p, c.c_void_p, c.c_int],
+        "sheep_ls_begin": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, c.c_uint32, u32p, vp, vp,
+                           vp, vp],
+        "sheep_ls_plan": [vp, vp, vp, vp],
+        "sheep_ls_map": [vp, c.c_uint32, vp, vp, vp, vp],
+        "sheep_ls_pack": [vp, c.c_uint32, vp, c.c_uint32, vp],
+        "sheep_ls_apply": [vp, c.c_uint32, vp, c.c_uint32, c.c_uint32, vp],
+        "sheep_ls_finish": [vp, u32p, u32p, u32p, c.c_int, u32p, u32p, vp],
+        "sheep_ls_free": [vp],
     }
     for name, args in sigs.items():
         f = getattr(L, name)

@@ -395,9 +395,10 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 
 // Buckets as unions of bins: K_e cuts at edge quantiles (exact bin counts) and K_r at rank
 // quantiles, each snapped to a bin bound.  bin_start: nb + 1 record offsets.
-static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
-                                 const std::vector<unsigned long long>& bin_start, uint64_t m,
-                                 uint32_t n_seq) {
+// The cuts as bin indices (sorted, distinct, in (0, nb - 1)).
+static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
+                                         const std::vector<unsigned long long>& bin_start,
+                                         uint64_t m, uint32_t n_seq) {
   const uint32_t nb = (uint32_t)bounds.size();
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
@@ -417,10 +418,18 @@ static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
   }
   std::sort(cuts.begin(), cuts.end());
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  return cuts;
+}
+
+static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
+                                 const std::vector<unsigned long long>& bin_start, uint64_t m,
+                                 uint32_t n_seq) {
+  const uint32_t nb = (uint32_t)bounds.size();
   Buckets bk;
   bk.emplace_back(0u, 0ull);
-  for (uint32_t i : cuts) bk.emplace_back(bounds[i], (uint64_t)bin_start[i]);
-  bk.emplace_back(n_seq, m_valid);
+  for (uint32_t i : bucket_cuts(bounds, bin_start, m, n_seq))
+    bk.emplace_back(bounds[i], (uint64_t)bin_start[i]);
+  bk.emplace_back(n_seq, (uint64_t)bin_start[nb - 1]);
   return bk;
 }
 
@@ -549,6 +558,223 @@ static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uin
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   tree_from_sorted(c, sorted, spare, m, n, lo_bit, d_parent, jump, nullptr, true, false, ws, s, tm);
   if (tm) tm->mark("tree_insert");
+}
+
+// ---- lockstep: the kb loop of ONE tree run by P ranks, each over its own edge shard --------
+// Every rank holds the same union-find, labels and forest.  Per bucket each rank maps only its
+// own records (the map is the part that scales with m), the kept pairs and giant marks of all
+// ranks are all-gathered by the caller (RCCL), and every rank applies the same union — the
+// zipper's result is the unique etree whatever the order, so the replicas stay identical.
+// Bins and buckets come from GLOBAL degrees and GLOBAL bin counts, hence agree on all ranks.
+struct Lockstep {
+  Scratch sc;  // own buffers: P sessions may share one device (the one-GPU simulation)
+  uint64_t m = 0;
+  uint32_t n_seq = 0;
+  std::vector<uint32_t> bounds;                // hi bins (global)
+  std::vector<unsigned long long> local_start;  // this shard's bin offsets, nb + 1
+  Buckets bk;                                   // (rank, local record offset)
+  std::vector<uint64_t> global_e;               // records per bucket over all ranks
+  uint32_t ms = 0;                              // mark slots (u64) per rank per bucket
+  uint32_t *bins = nullptr, *uf = nullptr, *label = nullptr, *linked = nullptr,
+           *counters = nullptr, *bitmap = nullptr, *spq = nullptr, *parent = nullptr,
+           *jump = nullptr, *hcnt = nullptr;
+  const uint64_t* sorted = nullptr;
+  unsigned long long* ws = nullptr;
+  uint32_t* h_pinned = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, apply_ev;
+  ~Lockstep() {
+    for (auto& e : map_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    for (auto& e : apply_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    if (h_pinned) (void)hipHostFree(h_pinned);
+    sc.release();
+  }
+  uint32_t anchor(size_t k) const { return (k >= 1 && bk[k].first > 0) ? bk[k].first - 1 : INV; }
+  std::pair<hipEvent_t, hipEvent_t> span(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
+                                         hipStream_t s) {
+    hipEvent_t a, b;
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&b));
+    HIP_CHECK(hipEventRecord(a, s));
+    v.emplace_back(a, b);
+    return v.back();
+  }
+};
+
+static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
+                     uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
+                     const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
+                     uint32_t* d_err, hipStream_t s) {
+  Scratch& sc = L.sc;
+  L.m = m;
+  L.n_seq = n_seq;
+  HIP_CHECK(hipHostMalloc(&L.h_pinned, 64, hipHostMallocDefault));
+  const size_t n = std::max<uint32_t>(n_seq, 1);
+  L.parent = (uint32_t*)sc.get("parent", n * 4);
+  L.jump = (uint32_t*)sc.get("jump", n * 4);
+  L.hcnt = (uint32_t*)sc.get("hcnt", n * 4);
+  L.uf = (uint32_t*)sc.get("uf", n * 4);
+  L.label = (uint32_t*)sc.get("label", n * 4);
+  L.linked = (uint32_t*)sc.get("linked", n * 4);
+  L.counters = (uint32_t*)sc.get("counters", 64);
+  const size_t bm_words = n / 32 + 2, spq_words = n / 32 + 64;
+  L.bitmap = (uint32_t*)sc.get("bitmap", bm_words * 4);
+  L.spq = (uint32_t*)sc.get("spq", spq_words * 4);
+  L.ws = (unsigned long long*)sc.get("ws", 128);
+  launch_fill(L.parent, INV, n, s);
+  launch_fill(L.jump, 0, n, s);
+  launch_fill(L.hcnt, 0, n, s);
+  launch_iota(L.uf, n, s);
+  launch_iota(L.label, n, s);
+  HIP_CHECK(hipMemsetAsync(L.counters, 0, 64, s));
+  HIP_CHECK(hipMemsetAsync(L.bitmap, 0, bm_words * 4, s));
+  HIP_CHECK(hipMemsetAsync(L.ws, 0, 128, s));
+  if (n_seq == 0) {
+    L.bounds.assign(1, 0u);
+    L.local_start.assign(2, 0ull);
+    L.local_start[1] = m;
+    *nb_out = 1;
+    counts_out[0] = m;
+    return;
+  }
+  // hi bins from the global degrees (identical on every rank)
+  const size_t nch = ((size_t)n_seq + 255) / 256;
+  uint64_t* cds = (uint64_t*)sc.get("chunk_deg", nch * 8);
+  launch_chunk_degsum(d_seq, d_deg, n_seq, cds, s);
+  std::vector<uint64_t> hd(nch);
+  HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.bounds = make_bins(hd, n_seq);
+  const uint32_t nb = (uint32_t)L.bounds.size();
+  L.bins = (uint32_t*)sc.get("bins", 512 * 4);
+  HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
+  // this shard's records -> items (hi, lo) grouped by bin
+  const uint64_t mm = std::max<uint64_t>(m, 1);
+  uint64_t* items = (uint64_t*)sc.get("items", mm * 8);
+  uint64_t* items_b = (uint64_t*)sc.get("items_b", mm * 8);
+  uint32_t* tmp = (uint32_t*)sc.get("rsort_tmp", rsort_tmp_words(mm) * 4);
+  uint16_t* digits = (uint16_t*)sc.get("item_bins", mm * 2);
+  const uint32_t* src = d_uv;
+  const bool part = m >= (1ull << 22);
+  if (part) {
+    uint32_t* pws = (uint32_t*)sc.get("part_ws", 1024 * 4);
+    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
+    src = (const uint32_t*)items_b;
+  }
+  launch_edge_pass_bins(src, m, d_rank, n_rank, items, d_err, L.bins, nb, tmp, digits, s, part);
+  unsigned long long* dstart = (unsigned long long*)sc.get("bin_start", 513 * 8);
+  if (m) {
+    bin_sort_u64(items, items_b, m, L.bins, nb, tmp, dstart, digits, s);
+    L.local_start.resize(nb + 1);
+    HIP_CHECK(hipMemcpyAsync(L.local_start.data(), dstart, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  } else {
+    L.local_start.assign(nb + 1, 0ull);
+  }
+  L.sorted = items_b;
+  for (uint32_t i = 0; i < nb; ++i) counts_out[i] = L.local_start[i + 1] - L.local_start[i];
+  *nb_out = nb;
+}
+
+static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_out,
+                    uint32_t* ms_out) {
+  const uint32_t nb = (uint32_t)L.bounds.size();
+  std::vector<unsigned long long> gstart(nb + 1, 0ull);
+  for (uint32_t i = 0; i < nb; ++i) gstart[i + 1] = gstart[i] + global_counts[i];
+  L.bk.clear();
+  L.global_e.clear();
+  L.ms = 0;
+  if (L.n_seq == 0) {
+    *nbk_out = 0;
+    *ms_out = 0;
+    return;
+  }
+  std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq);
+  std::vector<uint32_t> bi;  // bin index at each bucket start, then nb - 1 (the INVALID bin)
+  bi.push_back(0);
+  for (uint32_t i : cuts) bi.push_back(i);
+  bi.push_back(nb - 1);
+  for (size_t k = 0; k < bi.size(); ++k) {
+    const uint32_t r = k + 1 < bi.size() ? L.bounds[bi[k]] : L.n_seq;
+    L.bk.emplace_back(r, (uint64_t)L.local_start[bi[k]]);
+  }
+  for (size_t k = 0; k + 1 < bi.size(); ++k) {
+    L.global_e.push_back(gstart[bi[k + 1]] - gstart[bi[k]]);
+    const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
+    if (B1 > B0) L.ms = std::max<uint32_t>(L.ms, (((B1 - 1) >> 5) - (B0 >> 5) + 2) / 2);
+  }
+  *nbk_out = (uint32_t)L.global_e.size();
+  *ms_out = L.ms;
+}
+
+// d_count (nullable, device int64) receives the count without a host round trip;
+// n_kept_out (nullable) receives it on the host (synchronises).
+static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count,
+                   uint32_t* n_kept_out, hipStream_t s) {
+  if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
+  const uint32_t B0 = L.bk[k].first;
+  auto ev = L.span(L.map_ev, s);
+  launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
+                d_send + L.ms, L.bitmap, L.counters, 0, L.hcnt, false, L.ws, L.bins,
+                (uint32_t)L.bounds.size(), s);
+  HIP_CHECK(hipEventRecord(ev.second, s));
+  if (d_count) launch_ls_count(L.counters + 3, d_count, s);
+  if (n_kept_out) {
+    HIP_CHECK(hipMemcpyAsync(L.h_pinned, L.counters + 3, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    *n_kept_out = L.h_pinned[0];
+  }
+}
+
+static void ls_words(const Lockstep& L, uint32_t k, uint32_t* w0, uint32_t* w1) {
+  const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
+  *w0 = B0 >> 5;
+  *w1 = B1 > B0 ? (B1 - 1) >> 5 : B0 >> 5;
+}
+
+static void ls_pack(Lockstep& L, uint32_t k, uint64_t* d_send, uint32_t cap, hipStream_t s) {
+  if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
+  uint32_t w0, w1;
+  ls_words(L, k, &w0, &w1);
+  launch_ls_pack(L.bitmap, w0, w1, L.ms, d_send, L.counters + 3, cap, s);
+}
+
+static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P, uint32_t cap,
+                     hipStream_t s) {
+  if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
+  const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
+  uint32_t w0, w1;
+  ls_words(L, k, &w0, &w1);
+  uint64_t* kept = (uint64_t*)L.sc.get("kept_all", std::max<uint64_t>((uint64_t)P * cap, 1) * 8);
+  auto ev = L.span(L.apply_ev, s);
+  launch_ls_unpack(d_recv, P, L.ms, cap, L.bitmap, w0, w1, kept, L.counters + 3, s);
+  launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
+                  L.linked, L.bitmap, L.spq, L.counters, false, false, L.ws, s);
+  HIP_CHECK(hipEventRecord(ev.second, s));
+}
+
+static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t* d_deg,
+                      const uint32_t* d_selfc, int mode, uint32_t* d_parent, uint32_t* d_pst,
+                      hipStream_t s) {
+  if (L.n_seq) {
+    launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
+    HIP_CHECK(hipMemcpyAsync(d_parent, L.parent, (size_t)L.n_seq * 4, hipMemcpyDeviceToDevice, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  c.timings.clear();
+  c.span_names.clear();
+  auto sum = [&](const char* name, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+    double t = 0;
+    for (auto& e : v) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e.first, e.second);
+      t += ms;
+    }
+    c.timings.emplace_back(name, t);
+    c.span_names.push_back(std::string(name) + "#");
+    c.timings.emplace_back(c.span_names.back().c_str(), (double)v.size());
+  };
+  sum("kb_map", L.map_ev);
+  sum("kb_apply", L.apply_ev);
 }
 
 }  // namespace sheep
@@ -792,6 +1018,85 @@ int sheep_powerlaw_dev(uint32_t* d_uv, uint32_t n, double gamma, double i0, uint
   require_aligned(d_uv, "d_uv");
   if (n == 0 || !(gamma > 1.0) || !(i0 >= 0.0)) throw ApiError(-EINVAL, "powerlaw: n > 0, gamma > 1, i0 >= 0");
   launch_powerlaw(d_uv, n, gamma, i0, seed, e_begin, e_end, pick(c, stream));
+  API_END
+}
+
+// ---- lockstep multi-GPU tree build ---------------------------------------------------------
+
+int sheep_ls_begin(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_rank,
+                   const uint32_t* d_seq, uint32_t n_seq, const uint32_t* d_deg,
+                   uint64_t* bin_counts_out, uint32_t* n_bins_out, void** handle_out,
+                   void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (!bin_counts_out || !n_bins_out || !handle_out) throw ApiError(-EINVAL, "null output");
+  *handle_out = nullptr;
+  hipStream_t s = pick(c, stream);
+  Lockstep* L = new Lockstep();
+  try {
+    ls_begin(*L, d_uv, m, d_rank, n_rank, d_seq, n_seq, d_deg, bin_counts_out, n_bins_out,
+             c.d_err, s);
+    check_err(c, s);
+  } catch (...) {
+    delete L;
+    throw;
+  }
+  *handle_out = L;
+  API_END
+}
+
+int sheep_ls_plan(void* handle, const uint64_t* global_bin_counts, uint32_t* n_buckets_out,
+                  uint32_t* mark_slots_out) {
+  API_BEGIN
+  if (!handle || !global_bin_counts) throw ApiError(-EINVAL, "null argument");
+  ls_plan(*(Lockstep*)handle, global_bin_counts, n_buckets_out, mark_slots_out);
+  API_END
+}
+
+int sheep_ls_map(void* handle, uint32_t k, uint64_t* d_send, int64_t* d_count,
+                 uint32_t* n_kept_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!handle) throw ApiError(-EINVAL, "null handle");
+  ls_map(*(Lockstep*)handle, k, d_send, (long long*)d_count, n_kept_out, pick(c, stream));
+  API_END
+}
+
+int sheep_ls_pack(void* handle, uint32_t k, uint64_t* d_send, uint32_t cap, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!handle) throw ApiError(-EINVAL, "null handle");
+  ls_pack(*(Lockstep*)handle, k, d_send, cap, pick(c, stream));
+  API_END
+}
+
+int sheep_ls_apply(void* handle, uint32_t k, const uint64_t* d_recv, uint32_t n_ranks,
+                   uint32_t cap, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!handle || n_ranks == 0) throw ApiError(-EINVAL, "null handle or no ranks");
+  ls_apply(*(Lockstep*)handle, k, d_recv, n_ranks, cap, pick(c, stream));
+  API_END
+}
+
+int sheep_ls_finish(void* handle, const uint32_t* d_seq, const uint32_t* d_deg,
+                    const uint32_t* d_selfc, int degree_mode, uint32_t* d_parent, uint32_t* d_pst,
+                    void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!handle) throw ApiError(-EINVAL, "null handle");
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  hipStream_t s = pick(c, stream);
+  ls_finish(c, *(Lockstep*)handle, d_seq, d_deg, d_selfc, degree_mode, d_parent, d_pst, s);
+  check_err(c, s);
+  API_END
+}
+
+int sheep_ls_free(void* handle) {
+  API_BEGIN
+  delete (Lockstep*)handle;
   API_END
 }
 

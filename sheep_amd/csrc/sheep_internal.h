@@ -115,6 +115,14 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
                      bool refresh, bool stats, unsigned long long* st, hipStream_t s);
+// Lockstep exchange of one bucket (sheep_ls_*): pack this rank's mark words [w0, w1] (ms u64
+// slots) and kept pairs (padded to cap) for an all-gather; unpack P such blocks into the
+// bitmap (OR) and a contiguous kept array, setting *n_kept = P * cap.
+void launch_ls_pack(const uint32_t* bitmap, uint32_t w0, uint32_t w1, uint32_t ms, uint64_t* send,
+                    const uint32_t* n_kept /* device */, uint32_t cap, hipStream_t s);
+void launch_ls_count(const uint32_t* n_kept, long long* out, hipStream_t s);
+void launch_ls_unpack(const uint64_t* recv, uint32_t P, uint32_t ms, uint32_t cap, uint32_t* bitmap,
+                      uint32_t w0, uint32_t w1, uint64_t* kept, uint32_t* n_kept, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
 // Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)

@@ -1868,6 +1868,76 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      (const uint32_t*)parent, uf, label, B0, B1, counters);
 }
 
+// ---- lockstep exchange (multi-GPU kb loop, sheep_ls_*) -----------------------------------
+// One rank's contribution to a bucket, laid out for one all-gather: `ms` u64 slots holding the
+// bucket's mark words [w0, w1] (two per slot, zero beyond w1), then `cap` kept pairs, padded
+// past this rank's *d_kept (the map's count, cap >= it) with INVALID (b = INVALID: skipped by
+// the zipper).
+// The same rank's count as an int64 for the caller's MAX all-reduce.
+__global__ void k_ls_count(const uint32_t* __restrict__ n_kept, long long* out) { *out = *n_kept; }
+
+void launch_ls_count(const uint32_t* n_kept, long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_ls_count, dim3(1), dim3(1), 0, s, n_kept, out);
+}
+
+__global__ void k_ls_pack(const uint32_t* __restrict__ bitmap, uint32_t w0, uint32_t w1,
+                          uint32_t ms, uint64_t* send, const uint32_t* __restrict__ d_kept,
+                          uint32_t cap) {
+  const uint64_t total = (uint64_t)ms + cap;
+  const uint32_t n_kept = *d_kept;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i < ms) {
+      const uint32_t a = w0 + 2 * (uint32_t)i, b = a + 1;
+      const uint64_t lo = a <= w1 ? bitmap[a] : 0u, hi = b <= w1 ? bitmap[b] : 0u;
+      send[i] = lo | (hi << 32);
+    } else if (i - ms >= n_kept) {
+      send[i] = ~0ull;
+    }
+  }
+}
+
+// The all-gathered contributions of P ranks (P blocks of ms + cap slots): the mark words are
+// OR-ed over ranks into bitmap[w0, w1], the kept pairs copied to kept (P * cap, pads
+// included) and n_kept = P * cap.
+__global__ void k_ls_unpack(const uint64_t* __restrict__ recv, uint32_t P, uint32_t ms,
+                            uint32_t cap, uint32_t* bitmap, uint32_t w0, uint32_t w1,
+                            uint64_t* __restrict__ kept, uint32_t* n_kept) {
+  const uint64_t stride = (uint64_t)ms + cap;
+  const uint32_t nw = w1 - w0 + 1;
+  const uint64_t total = (uint64_t)nw + (uint64_t)P * cap;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i < nw) {
+      uint32_t v = 0;
+      for (uint32_t r = 0; r < P; ++r) {
+        const uint64_t s = recv[r * stride + (i >> 1)];
+        v |= (uint32_t)(i & 1 ? s >> 32 : s);
+      }
+      bitmap[w0 + i] = v;
+    } else {
+      const uint64_t j = i - nw, r = j / cap, q = j - r * cap;
+      kept[j] = recv[r * stride + ms + q];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_kept = P * cap;
+}
+
+void launch_ls_pack(const uint32_t* bitmap, uint32_t w0, uint32_t w1, uint32_t ms, uint64_t* send,
+                    const uint32_t* n_kept, uint32_t cap, hipStream_t s) {
+  const uint64_t total = (uint64_t)ms + cap;
+  if (total)
+    hipLaunchKernelGGL(k_ls_pack, dim3(grid_for(total)), dim3(BLOCK), 0, s, bitmap, w0, w1, ms, send,
+                       n_kept, cap);
+}
+
+void launch_ls_unpack(const uint64_t* recv, uint32_t P, uint32_t ms, uint32_t cap, uint32_t* bitmap,
+                      uint32_t w0, uint32_t w1, uint64_t* kept, uint32_t* n_kept, hipStream_t s) {
+  const uint64_t total = (uint64_t)(w1 - w0 + 1) + (uint64_t)P * cap;
+  hipLaunchKernelGGL(k_ls_unpack, dim3(grid_for(total)), dim3(BLOCK), 0, s, recv, P, ms, cap, bitmap,
+                     w0, w1, kept, n_kept);
+}
+
 // Items of one forest over n ranks for a union build: (parent[v] << 32 | v); a root's INVALID
 // parent becomes an INVALID hi, which sorts after every rank.
 __global__ void k_forest_items(const uint32_t* __restrict__ parent, uint32_t n,

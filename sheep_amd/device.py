@@ -109,6 +109,65 @@ def merge_forests(parents, n, out=None):
     return out
 
 
+class Lockstep:
+    """One rank's side of the lockstep multi-GPU tree build (sheep_ls_*, include/sheep_amd.h).
+    The collectives are the caller's (sheep_amd.dist.build_tree_lockstep)."""
+
+    def __init__(self, uv, rank, seq, n_seq, deg):
+        import numpy as np
+
+        self.m = uv.shape[0]
+        self.n_seq = n_seq
+        counts = np.zeros(513, np.uint64)
+        nb = ctypes.c_uint32(0)
+        h = ctypes.c_void_p()
+        capi.call("sheep_ls_begin", _p(uv), self.m, _p(rank), rank.numel(), _p(seq), n_seq,
+                  _p(deg), ctypes.c_void_p(counts.ctypes.data), ctypes.byref(nb),
+                  ctypes.byref(h), _stream())
+        self.h = h
+        self.bin_counts = counts[:nb.value].astype(np.int64)
+
+    def plan(self, global_counts):
+        """global_counts: this shard's bin_counts summed over ranks -> (buckets, mark slots)."""
+        import numpy as np
+
+        g = np.ascontiguousarray(np.asarray(global_counts, dtype=np.uint64))
+        nbk, ms = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        capi.call("sheep_ls_plan", self.h, ctypes.c_void_p(g.ctypes.data), ctypes.byref(nbk),
+                  ctypes.byref(ms))
+        self.slots = ms.value
+        return nbk.value, ms.value
+
+    def map(self, k, send, count=None):
+        """Map bucket k into send; with ``count`` (cuda int64 tensor) the kept-pair count is
+        written there (no synchronisation) and None returned, else it is returned."""
+        if count is not None:
+            capi.call("sheep_ls_map", self.h, k, _p(send), _p(count), None, _stream())
+            return None
+        n = ctypes.c_uint32(0)
+        capi.call("sheep_ls_map", self.h, k, _p(send), None, ctypes.byref(n), _stream())
+        return n.value
+
+    def pack(self, k, send, cap):
+        capi.call("sheep_ls_pack", self.h, k, _p(send), cap, _stream())
+
+    def apply(self, k, recv, n_ranks, cap):
+        capi.call("sheep_ls_apply", self.h, k, _p(recv), n_ranks, cap, _stream())
+
+    def finish(self, seq, deg_local, selfc, mode=capi.DEGREE_LLAMA):
+        dev = seq.device
+        parent = torch.empty(max(self.n_seq, 1), dtype=torch.uint32, device=dev)
+        pst = torch.empty(max(self.n_seq, 1), dtype=torch.uint32, device=dev)
+        capi.call("sheep_ls_finish", self.h, _p(seq), _p(deg_local), _p(selfc), mode, _p(parent),
+                  _p(pst), _stream())
+        return parent, pst
+
+    def free(self):
+        if self.h:
+            capi.call("sheep_ls_free", self.h)
+            self.h = None
+
+
 EVAL_KEYS = ("edges_cut", "vcom_vol", "vertex_bal", "ecv_hash", "hash_bal", "ecv_down",
              "down_bal", "ecv_up", "up_bal", "edges", "nodes")
 

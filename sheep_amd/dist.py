@@ -59,6 +59,133 @@ def build_tree_sharded(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     return seq, None, None, n_seq
 
 
+def _all_gather(recv, send, group):
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(recv, send, group=group)
+    else:
+        n = send.numel()
+        dist.all_gather([recv[r * n:(r + 1) * n] for r in range(recv.numel() // n)], send,
+                        group=group)
+
+
+def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
+    """graph2tree -i -r without partial trees (the default for P > 1).
+
+    Steps 1-2 as build_tree_sharded.  Then every rank bins ITS records by hi (bins from the
+    global degrees) and the ranks walk the kb rank buckets together: each maps its own records
+    of the bucket against its replica of the union-find, the kept pairs and giant marks of all
+    ranks are all-gathered over RCCL, and every rank applies all of them, so the replicas stay
+    identical and every rank ends with the whole elimination tree.  pst_weight is the sum of
+    the ranks' own pst (one sum-reduce to rank 0, as mpi_merge's merge adds them).
+    Returns (seq, parent, pst, n_seq) on rank 0 and (seq, parent, None, n_seq) elsewhere."""
+    import numpy as np
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    dev = uv_shard.device
+    deg_local, selfc = ops.degree(uv_shard, n_ids, mode)
+    deg = deg_local.clone() if world > 1 else deg_local
+    if world > 1:
+        dist.all_reduce(_i32(deg), op=dist.ReduceOp.SUM, group=group)
+    seq, rmap, n_seq = ops.sequence(deg)
+    ls = ops.lockstep(uv_shard, rmap, seq, n_seq, deg)
+    try:
+        counts = torch.from_numpy(np.ascontiguousarray(ls.bin_counts)).to(dev)
+        if world > 1:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        nbk, slots = ls.plan(counts.cpu().numpy())
+        if timings is not None:
+            timings["binned"] = ops.now()
+        send = torch.empty(slots + max(uv_shard.shape[0], 1), dtype=torch.int64, device=dev)
+        recv = torch.empty(0, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        for k in range(nbk):
+            if world > 1:  # one host round trip per bucket: the MAX of the kept counts
+                ls.map(k, send, cnt)
+                dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+                cap = int(cnt.item())
+            else:
+                cap = ls.map(k, send)
+            width = slots + cap
+            if send.numel() < width:  # another rank kept more pairs than this one has records
+                grown = torch.empty(width, dtype=torch.int64, device=dev)
+                grown[:send.numel()].copy_(send)
+                send = grown
+            ls.pack(k, send, cap)
+            if recv.numel() < world * width:
+                recv = torch.empty(world * width, dtype=torch.int64, device=dev)
+            if world > 1:
+                _all_gather(recv[:world * width], send[:width], group)
+            else:
+                recv[:width].copy_(send[:width])
+            ls.apply(k, recv, world, cap)
+        parent, pst = ls.finish(seq, deg_local, selfc, mode)
+    finally:
+        ls.free()
+    if timings is not None:
+        timings["tree"] = ops.now()
+    if world > 1:
+        dist.reduce(_i32(pst), dst=0, op=dist.ReduceOp.SUM, group=group)
+    return seq, parent, (pst if rank == 0 else None), n_seq
+
+
+def lockstep_local(shards, n_ids, mode=0, stats=None):
+    """The lockstep build of build_tree_lockstep for P shards held by ONE process on one
+    device (the all-gathers become device copies): the one-GPU rehearsal of the P-rank path.
+    stats (dict, optional) receives per-rank kernel times {"kb_map": [...], "kb_apply": [...]}.
+    Returns (seq, parent, pst, n_seq)."""
+    import numpy as np
+
+    from . import capi, device
+
+    P = len(shards)
+    dev = shards[0].device
+    parts = [device.degree_ex(uv, n_ids, mode) for uv in shards]
+    deg = parts[0][0].clone()
+    for d, _ in parts[1:]:
+        deg.view(torch.int32).add_(d.view(torch.int32))
+    seq, rmap, n_seq = device.sequence(deg)
+    sess = [device.Lockstep(uv, rmap, seq, n_seq, deg) for uv in shards]
+    try:
+        g = np.sum([s.bin_counts for s in sess], axis=0)
+        plans = [s.plan(g) for s in sess]
+        nbk, slots = plans[0]
+        sends = [torch.empty(slots + max(uv.shape[0], 1), dtype=torch.int64, device=dev)
+                 for uv in shards]
+        for k in range(nbk):
+            ns = [s.map(k, sends[r]) for r, s in enumerate(sess)]
+            cap = max(ns)
+            if stats is not None:
+                stats["kept"] = stats.get("kept", 0) + sum(ns)
+                stats["gathered"] = stats.get("gathered", 0) + P * cap
+            for r, s in enumerate(sess):
+                if sends[r].numel() < slots + cap:
+                    grown = torch.empty(slots + cap, dtype=torch.int64, device=dev)
+                    grown[:sends[r].numel()].copy_(sends[r])
+                    sends[r] = grown
+                s.pack(k, sends[r], cap)
+            recv = torch.cat([x[:slots + cap] for x in sends])
+            for s in sess:
+                s.apply(k, recv, P, cap)
+        pst = None
+        parent = None
+        for r, s in enumerate(sess):
+            p, w = s.finish(seq, parts[r][0], parts[r][1], mode)
+            if stats is not None:
+                for name, ms in capi.last_timings():
+                    stats.setdefault(name, []).append(ms)
+            if parent is None:
+                parent, pst = p, w
+            else:
+                if not torch.equal(parent[:n_seq], p[:n_seq]):
+                    raise RuntimeError("lockstep replicas diverged at rank %d" % r)
+                pst.view(torch.int32).add_(w.view(torch.int32))
+    finally:
+        for s in sess:
+            s.free()
+    return seq, parent, pst, n_seq
+
+
 class DeviceOps:
     """The HIP kernels behind the C-ABI, on torch's current stream."""
 
@@ -79,6 +206,9 @@ class DeviceOps:
 
         self.build_timings = capi.last_timings()  # this rank's partial tree, for the bench
         return out
+
+    def lockstep(self, uv, rmap, seq, n_seq, deg):
+        return self.d.Lockstep(uv, rmap, seq, n_seq, deg)
 
     def merge_into(self, pa, sa, pb, sb, n):
         self.d.merge_into(pa, sa, pb, sb, n)
