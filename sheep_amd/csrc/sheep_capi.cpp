@@ -575,12 +575,19 @@ struct Lockstep {
   Buckets bk;                                   // (rank, local record offset)
   std::vector<uint64_t> global_e;               // records per bucket over all ranks
   uint32_t ms = 0;                              // mark slots (u64) per rank per bucket
+  // Pipelined (default, SHEEP_LS_PIPE=0 turns it off): the caller maps (and exchanges) bucket
+  // k+1 while bucket k is applied, as the one-GPU loop does (tree_from_sorted): counters,
+  // marks and spine queues are double-buffered by bucket parity, the map of bucket k anchors
+  // the giant at the last rank of bucket k-2, and the apply refreshes the kept starts first.
+  bool pipe = true;
+  size_t bm_words = 0, spq_words = 0;
   uint32_t *bins = nullptr, *uf = nullptr, *label = nullptr, *linked = nullptr,
            *counters = nullptr, *bitmap = nullptr, *spq = nullptr, *parent = nullptr,
            *jump = nullptr, *hcnt = nullptr;
   const uint64_t* sorted = nullptr;
   unsigned long long* ws = nullptr;
   uint32_t* h_pinned = nullptr;
+  size_t kept_bytes = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, apply_ev;
   ~Lockstep() {
     for (auto& e : map_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -588,7 +595,13 @@ struct Lockstep {
     if (h_pinned) (void)hipHostFree(h_pinned);
     sc.release();
   }
-  uint32_t anchor(size_t k) const { return (k >= 1 && bk[k].first > 0) ? bk[k].first - 1 : INV; }
+  uint32_t anchor(size_t k) const {
+    const size_t a = pipe ? k - std::min<size_t>(k, 1) : k;
+    return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
+  }
+  uint32_t* cnt_of(size_t k) const { return counters + (pipe ? (k & 1) * 16 : 0); }
+  uint32_t* bm_of(size_t k) const { return bitmap + (pipe ? (k & 1) * bm_words : 0); }
+  uint32_t* spq_of(size_t k) const { return spq + (pipe ? (k & 1) * spq_words : 0); }
   std::pair<hipEvent_t, hipEvent_t> span(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
                                          hipStream_t s) {
     hipEvent_t a, b;
@@ -615,18 +628,22 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   L.uf = (uint32_t*)sc.get("uf", n * 4);
   L.label = (uint32_t*)sc.get("label", n * 4);
   L.linked = (uint32_t*)sc.get("linked", n * 4);
-  L.counters = (uint32_t*)sc.get("counters", 64);
+  const char* ep = getenv("SHEEP_LS_PIPE");
+  L.pipe = ep ? atoi(ep) != 0 : true;
+  L.counters = (uint32_t*)sc.get("counters", 2 * 64);
   const size_t bm_words = n / 32 + 2, spq_words = n / 32 + 64;
-  L.bitmap = (uint32_t*)sc.get("bitmap", bm_words * 4);
-  L.spq = (uint32_t*)sc.get("spq", spq_words * 4);
+  L.bm_words = bm_words;
+  L.spq_words = spq_words;
+  L.bitmap = (uint32_t*)sc.get("bitmap", 2 * bm_words * 4);
+  L.spq = (uint32_t*)sc.get("spq", 2 * spq_words * 4);
   L.ws = (unsigned long long*)sc.get("ws", 128);
   launch_fill(L.parent, INV, n, s);
   launch_fill(L.jump, 0, n, s);
   launch_fill(L.hcnt, 0, n, s);
   launch_iota(L.uf, n, s);
   launch_iota(L.label, n, s);
-  HIP_CHECK(hipMemsetAsync(L.counters, 0, 64, s));
-  HIP_CHECK(hipMemsetAsync(L.bitmap, 0, bm_words * 4, s));
+  HIP_CHECK(hipMemsetAsync(L.counters, 0, 2 * 64, s));
+  HIP_CHECK(hipMemsetAsync(L.bitmap, 0, 2 * bm_words * 4, s));
   HIP_CHECK(hipMemsetAsync(L.ws, 0, 128, s));
   if (n_seq == 0) {
     L.bounds.assign(1, 0u);
@@ -714,12 +731,12 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   const uint32_t B0 = L.bk[k].first;
   auto ev = L.span(L.map_ev, s);
   launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
-                d_send + L.ms, L.bitmap, L.counters, 0, L.hcnt, false, L.ws, L.bins,
+                d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws, L.bins,
                 (uint32_t)L.bounds.size(), s);
   HIP_CHECK(hipEventRecord(ev.second, s));
-  if (d_count) launch_ls_count(L.counters + 3, d_count, s);
+  if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
-    HIP_CHECK(hipMemcpyAsync(L.h_pinned, L.counters + 3, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(L.h_pinned, L.cnt_of(k) + 3, 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     *n_kept_out = L.h_pinned[0];
   }
@@ -735,7 +752,7 @@ static void ls_pack(Lockstep& L, uint32_t k, uint64_t* d_send, uint32_t cap, hip
   if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
   uint32_t w0, w1;
   ls_words(L, k, &w0, &w1);
-  launch_ls_pack(L.bitmap, w0, w1, L.ms, d_send, L.counters + 3, cap, s);
+  launch_ls_pack(L.bm_of(k), w0, w1, L.ms, d_send, L.cnt_of(k) + 3, cap, s);
 }
 
 static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P, uint32_t cap,
@@ -744,11 +761,17 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
   uint32_t w0, w1;
   ls_words(L, k, &w0, &w1);
-  uint64_t* kept = (uint64_t*)L.sc.get("kept_all", std::max<uint64_t>((uint64_t)P * cap, 1) * 8);
+  // a larger kept buffer replaces one that earlier applies may still read: drain first
+  const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
+  if (need > L.kept_bytes) {
+    HIP_CHECK(hipDeviceSynchronize());
+    L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
+  }
+  uint64_t* kept = (uint64_t*)L.sc.get("kept_all", L.kept_bytes);
   auto ev = L.span(L.apply_ev, s);
-  launch_ls_unpack(d_recv, P, L.ms, cap, L.bitmap, w0, w1, kept, L.counters + 3, s);
+  launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
-                  L.linked, L.bitmap, L.spq, L.counters, false, false, L.ws, s);
+                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, s);
   HIP_CHECK(hipEventRecord(ev.second, s));
 }
 

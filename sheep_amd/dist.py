@@ -68,6 +68,77 @@ def _all_gather(recv, send, group):
                         group=group)
 
 
+def _lockstep_loop(ls, nbk, slots, m_local, world, dev, group):
+    """Bucket by bucket: map, MAX of the kept counts, pack, all-gather, apply."""
+    send = torch.empty(slots + max(m_local, 1), dtype=torch.int64, device=dev)
+    recv = torch.empty(0, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    for k in range(nbk):
+        if world > 1:  # one host round trip per bucket: the MAX of the kept counts
+            ls.map(k, send, cnt)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+            cap = int(cnt.item())
+        else:
+            cap = ls.map(k, send)
+        width = slots + cap
+        if send.numel() < width:  # another rank kept more pairs than this one has records
+            grown = torch.empty(width, dtype=torch.int64, device=dev)
+            grown[:send.numel()].copy_(send)
+            send = grown
+        ls.pack(k, send, cap)
+        if recv.numel() < world * width:
+            recv = torch.empty(world * width, dtype=torch.int64, device=dev)
+        if world > 1:
+            _all_gather(recv[:world * width], send[:width], group)
+        else:
+            recv[:width].copy_(send[:width])
+        ls.apply(k, recv, world, cap)
+
+
+def _lockstep_loop_pipelined(ls, nbk, slots, m_local, world, dev, group):
+    """The same loop with bucket k+1 mapped and exchanged on a side stream while bucket k is
+    applied on the current one (the session double-buffers by bucket parity): the map and the
+    collectives hide behind the apply, which is the serial part."""
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    send = [torch.empty(slots + max(m_local, 1), dtype=torch.int64, device=dev)]
+    recv = [torch.empty(0, dtype=torch.int64, device=dev) for _ in range(2)]
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    applied = [torch.cuda.Event(), torch.cuda.Event()]
+    caps, ready = {}, {}
+
+    def produce(k):  # on the side stream; the host waits only for the count's MAX
+        with torch.cuda.stream(side):
+            ls.map(k, send[0], cnt)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+            cap = int(cnt.item())
+            width = slots + cap
+            if send[0].numel() < width:
+                grown = torch.empty(width, dtype=torch.int64, device=dev)
+                grown[:send[0].numel()].copy_(send[0])
+                send[0] = grown
+            ls.pack(k, send[0], cap)
+            r = recv[k & 1]
+            if r.numel() < world * width:
+                r = recv[k & 1] = torch.empty(world * width, dtype=torch.int64, device=dev)
+            _all_gather(r[:world * width], send[0][:width], group)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        caps[k], ready[k] = cap, ev
+
+    side.wait_stream(main)
+    produce(0)
+    for k in range(nbk):
+        main.wait_event(ready.pop(k))
+        ls.apply(k, recv[k & 1], world, caps.pop(k))
+        applied[k & 1].record(main)
+        if k + 1 < nbk:
+            if k >= 1:  # bucket k+1 reuses the parity buffers of bucket k-1
+                side.wait_event(applied[(k + 1) & 1])
+            produce(k + 1)
+    main.wait_stream(side)
+
+
 def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     """graph2tree -i -r without partial trees (the default for P > 1).
 
@@ -96,29 +167,10 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
         nbk, slots = ls.plan(counts.cpu().numpy())
         if timings is not None:
             timings["binned"] = ops.now()
-        send = torch.empty(slots + max(uv_shard.shape[0], 1), dtype=torch.int64, device=dev)
-        recv = torch.empty(0, dtype=torch.int64, device=dev)
-        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-        for k in range(nbk):
-            if world > 1:  # one host round trip per bucket: the MAX of the kept counts
-                ls.map(k, send, cnt)
-                dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
-                cap = int(cnt.item())
-            else:
-                cap = ls.map(k, send)
-            width = slots + cap
-            if send.numel() < width:  # another rank kept more pairs than this one has records
-                grown = torch.empty(width, dtype=torch.int64, device=dev)
-                grown[:send.numel()].copy_(send)
-                send = grown
-            ls.pack(k, send, cap)
-            if recv.numel() < world * width:
-                recv = torch.empty(world * width, dtype=torch.int64, device=dev)
-            if world > 1:
-                _all_gather(recv[:world * width], send[:width], group)
-            else:
-                recv[:width].copy_(send[:width])
-            ls.apply(k, recv, world, cap)
+        if world > 1 and dev.type == "cuda":
+            _lockstep_loop_pipelined(ls, nbk, slots, uv_shard.shape[0], world, dev, group)
+        else:
+            _lockstep_loop(ls, nbk, slots, uv_shard.shape[0], world, dev, group)
         parent, pst = ls.finish(seq, deg_local, selfc, mode)
     finally:
         ls.free()
