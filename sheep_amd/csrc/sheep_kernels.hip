@@ -1522,7 +1522,7 @@ __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
          int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode,
-         uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb) {
+         uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, int ro_find) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -1569,7 +1569,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
       uint32_t a = valid ? (uint32_t)it : 0u;
       uint32_t g = a;
       if (valid && a < B0 && mapmode != 2) {
-        const uint32_t rt = uf_find<false>(uf, a);
+        const uint32_t rt = ro_find ? uf_find_ro(uf, a) : uf_find<false>(uf, a);
         g = rt == RG ? G : label[rt];
       }
       // dedupe (mapmode 1): keep the first lane of every distinct (g, b) in the wave.  Off by
@@ -1730,10 +1730,32 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   }
 }
 
+// Giant fold (before k_kb_union): every marked rank of the bucket ends in the anchor's
+// component (the spine joins all of them to G), and its union-find slot is still its own
+// (iota: nothing links an in-bucket rank before its bucket's union), so it is stored under
+// that component's root R directly — no find, no CAS.  k_kb_union then skips the links
+// between two marked ranks (already in one tree).
+__global__ void k_kb_fold(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
+                          uint32_t* uf, uint32_t anchor) {
+  const uint32_t R = uf_find_ro(uf, anchor);
+  for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w <= ((B1 - 1) >> 5);
+       w += gridDim.x * blockDim.x) {
+    uint32_t bits = word_in(bitmap, w, B0, B1);
+    while (bits) {
+      const uint32_t v = (w << 5) + __ffs(bits) - 1;
+      bits &= bits - 1;
+      uf[v] = R;
+    }
+  }
+}
+
 // anchor: rank B0 - 1 (INV for the first bucket).  Its root R is never linked below another
 // root here, so the giant keeps one root from bucket to bucket: the map of the next bucket,
 // which runs concurrently in the pipelined loop, finds the same R from the same rank.  (All
 // threads read the same R: no union of this launch can move it.)
+// FOLD: k_kb_fold ran; links between two marked ranks are skipped, and the marks are cleared
+// by k_kb_label instead (this launch reads them).
+template <bool FOLD>
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
                            uint32_t B1, const uint32_t* __restrict__ linked,
                            const uint32_t* __restrict__ n_linked, uint32_t* bitmap,
@@ -1741,24 +1763,35 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
   const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
   // with the next bucket hold no marks of it yet; the previous bucket cleared its own)
-  for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
-       w += gridDim.x * blockDim.x)
-    bitmap[w] = 0;
+  if (!FOLD)
+    for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
+         w += gridDim.x * blockDim.x)
+      bitmap[w] = 0;
   const uint32_t nl = *n_linked, width = B1 - B0;
   const uint64_t total = (uint64_t)width + nl;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t v = i < width ? B0 + (uint32_t)i : linked[i - width];
     uint32_t p = parent[v];
-    if (p != INV) uf_union(uf, v, p, R);
+    if (p == INV) continue;
+    if (FOLD && i < width && p < B1 && ((bitmap[v >> 5] >> (v & 31)) & 1) &&
+        ((bitmap[p >> 5] >> (p & 31)) & 1))
+      continue;
+    uf_union(uf, v, p, R);
   }
 }
 
 // counters[1] = n_linked, [2] = n_spine, [3] = n_kept are reset here for the next bucket.
+// clear_marks: the bucket's marks are cleared here (FOLD: k_kb_union read them).
 __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
-                           uint32_t B0, uint32_t B1, uint32_t* counters) {
+                           uint32_t B0, uint32_t B1, uint32_t* counters, uint32_t* bitmap,
+                           int clear_marks) {
   for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
     if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
+  if (clear_marks)
+    for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
+         w += gridDim.x * blockDim.x)
+      bitmap[w] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) { counters[1] = 0; counters[2] = 0; counters[3] = 0; }
 }
 
@@ -1828,8 +1861,10 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
+  static const char* ef = getenv("SHEEP_KB_MAPFIND");
+  const int ro = ef && ef[0] == 'r';
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
-                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor, bins, nb);
+                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor, bins, nb, ro);
 }
 
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
@@ -1860,12 +1895,20 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
                        anchor, scan_limit, qchunk);
   }
+  // giant fold: the marks are relative to the anchor's component; its root R_a may later be
+  // linked below the union's R (pipelined: different anchors) — the folded ranks follow it
+  static const char* ef = getenv("SHEEP_KB_FOLD");
+  const bool fold = (ef ? atoi(ef) != 0 : true) && nonempty && anchor != INV && B1 > B0;
+  if (fold)
+    hipLaunchKernelGGL(k_kb_fold, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
+                       0, s, (const uint32_t*)bitmap, B0, B1, uf, anchor);
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
-  hipLaunchKernelGGL(k_kb_union, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
+  auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
+  hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,
                      B0 > 0 ? B0 - 1 : INV);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
-                     (const uint32_t*)parent, uf, label, B0, B1, counters);
+                     (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold);
 }
 
 // ---- lockstep exchange (multi-GPU kb loop, sheep_ls_*) -----------------------------------
