@@ -416,6 +416,28 @@ static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                             bounds.begin()) - 1;
     if (i > 0 && i < nb - 1) cuts.push_back(i);
   }
+  // Percolation window: where the records below rank r reach a mean degree 2E(r)/r of about
+  // 0.25..1.5, the giant component forms inside a bucket, and with no union-find help inside
+  // the bucket the zipper's walks get long (RMAT-26: two such buckets held 4 of the 14 ms of
+  // zipper time, 19 steps per edge against ~1.05 elsewhere).  Buckets there are cut TR times
+  // finer than the rank quantiles (SHEEP_KB_TRANS, 0 = off).  E(r) is exact at bin bounds.
+  // Measured and OFF by default: the window holds far more buckets than the two slow ones
+  // (RMAT-26 95 -> 129 buckets: 77.2 -> 84.5 ms; LJ-shape 7.6 -> 9.1 ms).
+  const char* et = getenv("SHEEP_KB_TRANS");
+  const uint32_t TR = et ? (uint32_t)atoi(et) : 0;
+  if (TR > 1) {
+    const uint64_t spacing = std::max<uint64_t>(1, (uint64_t)n_seq / ((uint64_t)K_r * TR));
+    uint64_t last = ~0ull;
+    for (uint32_t i = 1; i + 1 < nb; ++i) {
+      const double r = (double)bounds[i], dens = r > 0 ? 2.0 * (double)bin_start[i] / r : 0.0;
+      if (dens < 0.25 || dens > 1.5) continue;
+      const uint64_t slot = bounds[i] / spacing;
+      if (slot != last) {
+        cuts.push_back(i);
+        last = slot;
+      }
+    }
+  }
   std::sort(cuts.begin(), cuts.end());
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
   return cuts;
