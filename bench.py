@@ -104,6 +104,9 @@ def main():
     # merge (per-rank partial trees, gathered and merged on rank 0)
     ap.add_argument("--dist", default=os.environ.get("SHEEP_DIST", "lockstep"),
                     choices=["lockstep", "merge"])
+    # N = 1 through the N > 1 code: the lockstep loop over a one-rank process group (RCCL), to
+    # measure its host overhead and collective launches on one GPU (not the default N = 1 path)
+    ap.add_argument("--lockstep-1", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,8 +117,11 @@ def main():
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.lockstep_1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -151,6 +157,8 @@ def main():
         torch.cuda.synchronize()
 
     def step():
+        if world == 1 and args.lockstep_1:
+            return build_tree_lockstep(uv, n_ids, ops)
         if world == 1:
             return device.graph2tree(uv, n_ids)
         if args.dist == "lockstep":
@@ -166,7 +174,7 @@ def main():
         out = step()
         # N > 1: the partial-tree build of this rank (the merge's own phases are "merge_*")
         tl = capi.last_timings()
-        if world > 1 and args.dist == "merge":
+        if world > 1 and args.dist == "merge" and not args.lockstep_1:
             tl = list(ops.build_timings) + [("merge_" + k, v) for k, v in tl]
         for name, ms in tl:
             phase.setdefault(name, []).append(ms)
@@ -234,7 +242,7 @@ def main():
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
             rec["cpu_baseline_ir"] = cpu_baseline_ir(args.cpu_scale, ef, args.cpu_scale, threads)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -60,6 +60,12 @@ void* Scratch::get(const char* name, size_t bytes) {
   return sl.p;
 }
 
+size_t Scratch::bytes_of(const char* name) const {
+  for (auto& s : slots)
+    if (s.first == name) return s.second.bytes;
+  return 0;
+}
+
 void Scratch::release() {
   for (auto& s : slots)
     if (s.second.p) (void)hipFree(s.second.p);
@@ -589,7 +595,12 @@ static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uin
 // zipper's result is the unique etree whatever the order, so the replicas stay identical.
 // Bins and buckets come from GLOBAL degrees and GLOBAL bin counts, hence agree on all ranks.
 struct Lockstep {
-  Scratch sc;  // own buffers: P sessions may share one device (the one-GPU simulation)
+  // Buffers: the device's scratch (kept across calls, like every other entry point) for the
+  // first live session; a private one for further concurrent sessions on the same device (the
+  // one-GPU simulation of P ranks).
+  Ctx* ctx = nullptr;
+  Scratch own;
+  Scratch* scp = nullptr;
   uint64_t m = 0;
   uint32_t n_seq = 0;
   std::vector<uint32_t> bounds;                // hi bins (global)
@@ -597,11 +608,11 @@ struct Lockstep {
   Buckets bk;                                   // (rank, local record offset)
   std::vector<uint64_t> global_e;               // records per bucket over all ranks
   uint32_t ms = 0;                              // mark slots (u64) per rank per bucket
-  // Pipelined (default, SHEEP_LS_PIPE=0 turns it off): the caller maps (and exchanges) bucket
-  // k+1 while bucket k is applied, as the one-GPU loop does (tree_from_sorted): counters,
-  // marks and spine queues are double-buffered by bucket parity, the map of bucket k anchors
-  // the giant at the last rank of bucket k-2, and the apply refreshes the kept starts first.
-  bool pipe = true;
+  // Pipelined: the caller may map (and exchange) bucket k+1 while bucket k is applied, as the
+  // one-GPU loop does (tree_from_sorted): counters, marks and spine queues are double-buffered
+  // by bucket parity, the map of bucket k anchors the giant at the last rank of bucket k-2, and
+  // the apply refreshes the kept starts first.  Exact for any interleaving of the two.
+  static constexpr bool pipe = true;
   size_t bm_words = 0, spq_words = 0;
   uint32_t *bins = nullptr, *uf = nullptr, *label = nullptr, *linked = nullptr,
            *counters = nullptr, *bitmap = nullptr, *spq = nullptr, *parent = nullptr,
@@ -615,7 +626,8 @@ struct Lockstep {
     for (auto& e : map_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     for (auto& e : apply_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (h_pinned) (void)hipHostFree(h_pinned);
-    sc.release();
+    own.release();
+    if (ctx) ctx->ls_live--;
   }
   uint32_t anchor(size_t k) const {
     const size_t a = pipe ? k - std::min<size_t>(k, 1) : k;
@@ -639,26 +651,24 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
                      uint32_t* d_err, hipStream_t s) {
-  Scratch& sc = L.sc;
+  Scratch& sc = *L.scp;
   L.m = m;
   L.n_seq = n_seq;
   HIP_CHECK(hipHostMalloc(&L.h_pinned, 64, hipHostMallocDefault));
   const size_t n = std::max<uint32_t>(n_seq, 1);
-  L.parent = (uint32_t*)sc.get("parent", n * 4);
-  L.jump = (uint32_t*)sc.get("jump", n * 4);
-  L.hcnt = (uint32_t*)sc.get("hcnt", n * 4);
-  L.uf = (uint32_t*)sc.get("uf", n * 4);
-  L.label = (uint32_t*)sc.get("label", n * 4);
-  L.linked = (uint32_t*)sc.get("linked", n * 4);
-  const char* ep = getenv("SHEEP_LS_PIPE");
-  L.pipe = ep ? atoi(ep) != 0 : true;
-  L.counters = (uint32_t*)sc.get("counters", 2 * 64);
+  L.parent = (uint32_t*)sc.get("ls_parent", n * 4);
+  L.jump = (uint32_t*)sc.get("ls_jump", n * 4);
+  L.hcnt = (uint32_t*)sc.get("ls_hcnt", n * 4);
+  L.uf = (uint32_t*)sc.get("ls_uf", n * 4);
+  L.label = (uint32_t*)sc.get("ls_label", n * 4);
+  L.linked = (uint32_t*)sc.get("ls_linked", n * 4);
+  L.counters = (uint32_t*)sc.get("ls_counters", 2 * 64);
   const size_t bm_words = n / 32 + 2, spq_words = n / 32 + 64;
   L.bm_words = bm_words;
   L.spq_words = spq_words;
-  L.bitmap = (uint32_t*)sc.get("bitmap", 2 * bm_words * 4);
-  L.spq = (uint32_t*)sc.get("spq", 2 * spq_words * 4);
-  L.ws = (unsigned long long*)sc.get("ws", 128);
+  L.bitmap = (uint32_t*)sc.get("ls_bitmap", 2 * bm_words * 4);
+  L.spq = (uint32_t*)sc.get("ls_spq", 2 * spq_words * 4);
+  L.ws = (unsigned long long*)sc.get("ls_ws", 128);
   launch_fill(L.parent, INV, n, s);
   launch_fill(L.jump, 0, n, s);
   launch_fill(L.hcnt, 0, n, s);
@@ -677,30 +687,30 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   }
   // hi bins from the global degrees (identical on every rank)
   const size_t nch = ((size_t)n_seq + 255) / 256;
-  uint64_t* cds = (uint64_t*)sc.get("chunk_deg", nch * 8);
+  uint64_t* cds = (uint64_t*)sc.get("ls_chunk_deg", nch * 8);
   launch_chunk_degsum(d_seq, d_deg, n_seq, cds, s);
   std::vector<uint64_t> hd(nch);
   HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   L.bounds = make_bins(hd, n_seq);
   const uint32_t nb = (uint32_t)L.bounds.size();
-  L.bins = (uint32_t*)sc.get("bins", 512 * 4);
+  L.bins = (uint32_t*)sc.get("ls_bins", 512 * 4);
   HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
   // this shard's records -> items (hi, lo) grouped by bin
   const uint64_t mm = std::max<uint64_t>(m, 1);
-  uint64_t* items = (uint64_t*)sc.get("items", mm * 8);
-  uint64_t* items_b = (uint64_t*)sc.get("items_b", mm * 8);
-  uint32_t* tmp = (uint32_t*)sc.get("rsort_tmp", rsort_tmp_words(mm) * 4);
-  uint16_t* digits = (uint16_t*)sc.get("item_bins", mm * 2);
+  uint64_t* items = (uint64_t*)sc.get("ls_items", mm * 8);
+  uint64_t* items_b = (uint64_t*)sc.get("ls_items_b", mm * 8);
+  uint32_t* tmp = (uint32_t*)sc.get("ls_rsort_tmp", rsort_tmp_words(mm) * 4);
+  uint16_t* digits = (uint16_t*)sc.get("ls_item_bins", mm * 2);
   const uint32_t* src = d_uv;
   const bool part = m >= (1ull << 22);
   if (part) {
-    uint32_t* pws = (uint32_t*)sc.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", 1024 * 4);
     launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
     src = (const uint32_t*)items_b;
   }
   launch_edge_pass_bins(src, m, d_rank, n_rank, items, d_err, L.bins, nb, tmp, digits, s, part);
-  unsigned long long* dstart = (unsigned long long*)sc.get("bin_start", 513 * 8);
+  unsigned long long* dstart = (unsigned long long*)sc.get("ls_bin_start", 513 * 8);
   if (m) {
     bin_sort_u64(items, items_b, m, L.bins, nb, tmp, dstart, digits, s);
     L.local_start.resize(nb + 1);
@@ -785,11 +795,12 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   ls_words(L, k, &w0, &w1);
   // a larger kept buffer replaces one that earlier applies may still read: drain first
   const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
+  if (L.kept_bytes == 0) L.kept_bytes = L.scp->bytes_of("ls_kept_all");
   if (need > L.kept_bytes) {
     HIP_CHECK(hipDeviceSynchronize());
     L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
   }
-  uint64_t* kept = (uint64_t*)L.sc.get("kept_all", L.kept_bytes);
+  uint64_t* kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
   auto ev = L.span(L.apply_ev, s);
   launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
@@ -1079,6 +1090,8 @@ int sheep_ls_begin(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uin
   *handle_out = nullptr;
   hipStream_t s = pick(c, stream);
   Lockstep* L = new Lockstep();
+  L->ctx = &c;
+  L->scp = c.ls_live++ == 0 ? &c.scratch : &L->own;
   try {
     ls_begin(*L, d_uv, m, d_rank, n_rank, d_seq, n_seq, d_deg, bin_counts_out, n_bins_out,
              c.d_err, s);

@@ -22,6 +22,7 @@ struct Scratch {
   struct Slot { void* p = nullptr; size_t bytes = 0; };
   std::vector<std::pair<std::string, Slot>> slots;
   void* get(const char* name, size_t bytes);  // throws std::runtime_error on hipMalloc failure
+  size_t bytes_of(const char* name) const;    // current size of a slot (0: none)
   void release();
 };
 
@@ -35,6 +36,7 @@ struct Ctx {
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
   std::vector<std::pair<const char*, double>> timings;
   std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
+  int ls_live = 0;                     // live lockstep sessions (sheep_ls_*) on this device
 };
 
 Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)

@@ -167,7 +167,7 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
         nbk, slots = ls.plan(counts.cpu().numpy())
         if timings is not None:
             timings["binned"] = ops.now()
-        if world > 1 and dev.type == "cuda":
+        if dist.is_initialized() and dev.type == "cuda":
             _lockstep_loop_pipelined(ls, nbk, slots, uv_shard.shape[0], world, dev, group)
         else:
             _lockstep_loop(ls, nbk, slots, uv_shard.shape[0], world, dev, group)
