@@ -105,7 +105,8 @@ def _lockstep_loop_pipelined(ls, nbk, slots, m_local, world, dev, group):
     recv = [torch.empty(0, dtype=torch.int64, device=dev) for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     applied = [torch.cuda.Event(), torch.cuda.Event()]
-    caps, ready = {}, {}
+    exchanged = [torch.cuda.Event(), torch.cuda.Event()]
+    caps = {}
 
     def produce(k):  # on the side stream; the host waits only for the count's MAX
         with torch.cuda.stream(side):
@@ -122,14 +123,13 @@ def _lockstep_loop_pipelined(ls, nbk, slots, m_local, world, dev, group):
             if r.numel() < world * width:
                 r = recv[k & 1] = torch.empty(world * width, dtype=torch.int64, device=dev)
             _all_gather(r[:world * width], send[0][:width], group)
-            ev = torch.cuda.Event()
-            ev.record(side)
-        caps[k], ready[k] = cap, ev
+            exchanged[k & 1].record(side)
+        caps[k] = cap
 
     side.wait_stream(main)
     produce(0)
     for k in range(nbk):
-        main.wait_event(ready.pop(k))
+        main.wait_event(exchanged[k & 1])
         ls.apply(k, recv[k & 1], world, caps.pop(k))
         applied[k & 1].record(main)
         if k + 1 < nbk:
