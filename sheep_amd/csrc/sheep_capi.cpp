@@ -238,10 +238,13 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 
 // kb bucket counts: each bucket costs a fixed ~60-100 us of launches and small kernels, while
 // too few buckets leave the zipper long in-bucket walks (profiles/r01/kb_bucket_sweep.txt).
-static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r) {
+// kmax: 64 for the one-GPU loop (its map, on the critical path, wants short buckets); the
+// lockstep loop's critical path is the apply, whose per-bucket cost favours fewer buckets
+// (RMAT-26, P = 8 simulation: K = 40/48/56/64 -> apply 18.8/18.7/19.2/20.5 ms).
+static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 64) {
   const char* ek = getenv("SHEEP_KB_BUCKETS");
   const char* er = getenv("SHEEP_KB_RANKB");
-  const uint32_t K_auto = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, m >> 23));
+  const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
   *K_e = ek ? (uint32_t)atoi(ek) : K_auto;
   *K_r = er ? (uint32_t)atoi(er) : K_auto;
 }
@@ -404,11 +407,11 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 // The cuts as bin indices (sorted, distinct, in (0, nb - 1)).
 static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                                          const std::vector<unsigned long long>& bin_start,
-                                         uint64_t m, uint32_t n_seq) {
+                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 64) {
   const uint32_t nb = (uint32_t)bounds.size();
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
-  kb_counts(m, &K_e, &K_r);
+  kb_counts(m, &K_e, &K_r, kmax);
   std::vector<uint32_t> cuts;
   for (uint32_t k = 1; k < K_e; ++k) {
     const uint64_t target = m_valid * k / K_e;
@@ -737,7 +740,7 @@ static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_ou
     *ms_out = 0;
     return;
   }
-  std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq);
+  std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq, 40);
   std::vector<uint32_t> bi;  // bin index at each bucket start, then nb - 1 (the INVALID bin)
   bi.push_back(0);
   for (uint32_t i : cuts) bi.push_back(i);
