@@ -30,3 +30,19 @@ def test_abi_version_and_error_text_without_gpu():
     L = capi.lib()
     assert L.sheep_abi_version() >> 16 == 1
     assert isinstance(L.sheep_last_error(), bytes)
+
+
+def test_lockstep_entry_points_reject_null_handles_without_gpu():
+    """The lockstep calls validate their handle before touching a device (sheep_ls_*)."""
+    import ctypes
+    import errno
+
+    L = capi.lib()
+    for s in ("sheep_ls_begin", "sheep_ls_plan", "sheep_ls_map", "sheep_ls_pack", "sheep_ls_apply",
+              "sheep_ls_finish", "sheep_ls_free"):
+        assert s in capi.header_symbols()
+    n = ctypes.c_uint32(0)
+    counts = (ctypes.c_uint64 * 4)()
+    assert L.sheep_ls_plan(None, counts, ctypes.byref(n), ctypes.byref(n)) == -errno.EINVAL
+    assert b"null" in L.sheep_last_error()
+    assert L.sheep_ls_free(None) == 0
