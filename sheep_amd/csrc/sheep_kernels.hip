@@ -618,7 +618,10 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
     counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
-template <int DB, bool BINS = false>
+// TM: offsets are tile-major (offsets[tile * NBIN + digit], see k_tm_rows) instead of
+// digit-major (offsets[digit * ntiles + tile]): the tile reads its NBIN offsets as one
+// contiguous run instead of NBIN scattered words.
+template <int DB, bool BINS = false, bool TM = false>
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n, int shift,
                 const uint32_t* __restrict__ offsets, uint32_t ntiles,
@@ -639,7 +642,8 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : RS_TILE);
   const uint32_t wbase = (uint32_t)w * (64 * RS_ITEMS) + lane;  // tile index of round 0
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (uint32_t i = t; i < NBIN; i += RS_THREADS) goff[i] = offsets[(uint64_t)i * ntiles + blockIdx.x];
+  for (uint32_t i = t; i < NBIN; i += RS_THREADS)
+    goff[i] = TM ? offsets[(uint64_t)blockIdx.x * NBIN + i] : offsets[(uint64_t)i * ntiles + blockIdx.x];
   for (uint32_t i = lane; i < NBIN; i += 64) whist[w][i] = 0;
   if (BINS) {
     for (uint32_t i = t; i < nb; i += RS_THREADS) sb[i] = bins[i];
@@ -708,11 +712,96 @@ __global__ void k_bin_starts(const uint32_t* __restrict__ offsets, uint32_t ntil
     bin_start[d] = d < nb ? offsets[(uint64_t)d * ntiles] : n;
 }
 
+// Tile-major bin counts (counts[tile * 512 + bin], written by k_edge_pass_tiles<..., TM>) ->
+// tile-major global offsets, in three coalesced passes over groups of TM_G tiles:
+//   k_tm_colsum       gsum[g][bin] = records of the bin in group g;
+//   k_tm_scan_groups  gsum[g][bin] <- exclusive prefix over groups; bin_start = exclusive
+//                     prefix of the bin totals (and n at [nb]);
+//   k_tm_rows         counts[t][bin] <- bin_start[bin] + gsum[g][bin] + earlier tiles of g.
+// The digit-major layout had every tile write (edge pass) and read (scatter) 512 words that
+// lie ntiles words apart: 131 K tiles x 512 x a 64-B sector each way at RMAT-26.
+static constexpr uint32_t TM_G = 256;  // tiles per group
+
+__global__ void __launch_bounds__(512)
+k_tm_colsum(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ gsum) {
+  const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
+  uint32_t sum = 0;
+  for (uint32_t t = t0; t < t1; t += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? counts[(uint64_t)(t + u) * 512 + d] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += v[u];
+  }
+  gsum[(uint64_t)blockIdx.x * 512 + d] = sum;
+}
+
+__global__ void __launch_bounds__(512)
+k_tm_scan_groups(uint32_t* __restrict__ gsum, uint32_t ngroups, uint32_t nb, uint64_t n,
+                 unsigned long long* __restrict__ bin_start) {
+  __shared__ uint32_t wsum[8];
+  const uint32_t d = threadIdx.x, lane = d & 63, w = d >> 6;
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < ngroups; g += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = g + u < ngroups ? gsum[(uint64_t)(g + u) * 512 + d] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (g + u < ngroups) gsum[(uint64_t)(g + u) * 512 + d] = run;
+      run += v[u];
+    }
+  }
+  const uint32_t incl = wave_incl_scan(run);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t i = 0; i < w; ++i) add += wsum[i];
+  if (d < nb) bin_start[d] = add + incl - run;
+  if (d == 0) bin_start[nb] = n;
+}
+
+__global__ void __launch_bounds__(512)
+k_tm_rows(uint32_t* __restrict__ counts, uint32_t ntiles, const uint32_t* __restrict__ gsum,
+          const unsigned long long* __restrict__ bin_start, uint32_t nb) {
+  const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
+  uint32_t run = (d < nb ? (uint32_t)bin_start[d] : 0u) + gsum[(uint64_t)blockIdx.x * 512 + d];
+  for (uint32_t t = t0; t < t1; t += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? counts[(uint64_t)(t + u) * 512 + d] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (t + u < t1) counts[(uint64_t)(t + u) * 512 + d] = run;
+      run += v[u];
+    }
+  }
+}
+
+// SHEEP_BIN_TM=0: the digit-major counts and one flat scan (the previous layout).
+static bool bin_tile_major() {
+  static const char* e = getenv("SHEEP_BIN_TM");
+  return e ? atoi(e) != 0 : true;
+}
+
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
                   uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
                   hipStream_t s) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
+  if (bin_tile_major()) {
+    const uint32_t ng = (uint32_t)((nt + TM_G - 1) / TM_G);
+    uint32_t* gsum = tmp + 512 * nt;
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_tm_colsum, dim3(ng), dim3(512), 0, s, (const uint32_t*)counts, (uint32_t)nt,
+                       gsum);
+    hipLaunchKernelGGL(k_tm_scan_groups, dim3(1), dim3(512), 0, s, gsum, ng, nb, n, bin_start);
+    hipLaunchKernelGGL(k_tm_rows, dim3(ng), dim3(512), 0, s, counts, (uint32_t)nt,
+                       (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb);
+    hipLaunchKernelGGL((k_rsort_scatter<9, true, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in,
+                       out, n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
+    return;
+  }
   uint32_t* stmp = tmp + 512 * nt;
   launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
   hipLaunchKernelGGL(k_bin_starts, dim3(3), dim3(BLOCK), 0, s, (const uint32_t*)counts, (uint32_t)nt,
@@ -724,7 +813,7 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
 
 size_t rsort_tmp_words(uint64_t n) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
-  return 512 * nt + scan_tmp_words(512 * nt);
+  return 512 * nt + std::max<size_t>(scan_tmp_words(512 * nt), 512 * ((nt + TM_G - 1) / TM_G));
 }
 
 // Digit width of the first pass when `bits` are sorted in passes of <= 9 bits (even split,
@@ -899,7 +988,8 @@ void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_se
 constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
 constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
 
-template <int DB, bool PRE, bool BINS = false>
+// TM: the tile histograms are written tile-major (bin_sort_u64's k_tm_* passes).
+template <int DB, bool PRE, bool BINS = false, bool TM = false>
 __global__ void __launch_bounds__(RS_THREADS)
 k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
                   uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
@@ -960,7 +1050,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
   }
   __syncthreads();
   for (uint32_t i = t; i < NBIN; i += RS_THREADS)
-    counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
+    counts[TM ? (uint64_t)blockIdx.x * NBIN + i : (uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
 // Edge pass whose output feeds radix_sort_u64(..., bit_lo = shift, counted0 = true): tmp is
@@ -971,8 +1061,10 @@ void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank,
                            uint32_t* tmp, uint16_t* digits, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
-  if (nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
-  auto k = pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>;
+  const bool tm = bin_tile_major();  // every tile writes all 512 of its counts
+  if (!tm && nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
+  auto k = tm ? (pre ? k_edge_pass_tiles<9, true, true, true> : k_edge_pass_tiles<9, false, true, true>)
+              : (pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
                      (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits);
 }
