@@ -265,6 +265,11 @@ void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32
 // Supports n_ids <= 2^26 (launch_degree_bucketed falls back to k_degree above that).
 // ---------------------------------------------------------------------------------------
 static constexpr int DEGB_THREADS = 1024;
+// Tile-major count matrices and their scan (defined with the hi bins below).
+static bool bin_tile_major();
+static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
+                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s);
+static constexpr uint32_t TM_G = 256;  // tiles per group
 static constexpr int DEGB_CHUNK = 32768;  // edges per chunk (<= 65536 endpoints -> 128 KB LDS)
 static constexpr uint32_t DEGB_NB = 1024;
 static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgroup
@@ -275,7 +280,7 @@ __device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
              uint32_t NB, uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t* err,
-             int psh, uint32_t* __restrict__ yhist) {
+             int psh, uint32_t* __restrict__ yhist, int tm) {
   __shared__ uint32_t hist[DEGB_NB];
   __shared__ uint32_t yh[256];  // y digits of the later rank-gather partition (nullable yhist)
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
@@ -306,13 +311,13 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
       if (yh[i]) atomicAdd(&yhist[i], yh[i]);
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x)
-    counts[(uint64_t)i * nchunks + blockIdx.x] = hist[i];
+    counts[tm ? (uint64_t)blockIdx.x * NB + i : (uint64_t)i * nchunks + blockIdx.x] = hist[i];
 }
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
                uint32_t NB, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
-               uint32_t nchunks, uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc) {
+               uint32_t nchunks, uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc, int tm) {
   __shared__ uint32_t cur[DEGB_NB], start[DEGB_NB], goff[DEGB_NB], wsum[DEGB_THREADS / 64];
   __shared__ uint16_t buf[2 * DEGB_CHUNK];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -320,8 +325,9 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
   // this chunk's bucket counts and global run offsets (one scattered read per thread)
   uint32_t cnt = 0;
   if (t < (int)NB) {
-    cnt = counts[(uint64_t)t * nchunks + blockIdx.x];
-    goff[t] = offsets[(uint64_t)t * nchunks + blockIdx.x];
+    const uint64_t at = tm ? (uint64_t)blockIdx.x * NB + t : (uint64_t)t * nchunks + blockIdx.x;
+    cnt = counts[at];
+    goff[t] = offsets[at];
   }
   uint32_t incl = wave_incl_scan(cnt);
   if (lane == 63) wsum[w] = incl;
@@ -366,15 +372,18 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
-            uint32_t n_ids, uint32_t* __restrict__ deg) {
+            uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
-  uint64_t s0 = offsets[(uint64_t)b * nchunks];
+  // bstart (tile-major counts): bucket starts and the total; else the digit-major offsets
   const uint64_t last = (uint64_t)NB * nchunks - 1;
-  uint64_t s1 = (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks] : (uint64_t)offsets[last] + counts[last];
+  uint64_t s0 = bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
+  uint64_t s1 = bstart ? bstart[b + 1]
+                       : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                      : (uint64_t)offsets[last] + counts[last];
   const int lane = threadIdx.x & 63;
   // 32 entries (four 16-B loads, all issued before use: the loop is latency-bound otherwise)
   // per thread per iteration, from the 8-aligned entry below s0 (ep is padded: the loads may
@@ -424,14 +433,15 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
               const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, uint32_t n_ids,
-              uint32_t* __restrict__ deg) {
+              uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const uint64_t s0 = offsets[(uint64_t)b * nchunks];
   const uint64_t last = (uint64_t)NB * nchunks - 1;
-  const uint64_t s1 = (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
-                                   : (uint64_t)offsets[last] + counts[last];
+  const uint64_t s0 = bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
+  const uint64_t s1 = bstart ? bstart[b + 1]
+                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                            : (uint64_t)offsets[last] + counts[last];
   uint32_t acc[64];
 #pragma unroll
   for (int k = 0; k < 64; ++k) acc[k] = 0;
@@ -497,6 +507,10 @@ static bool degb_params(uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
   return true;
 }
 
+static size_t degb_scan_words(uint64_t cw, uint64_t nchunks, uint32_t NB) {
+  return std::max<size_t>(scan_tmp_words(cw), NB * ((nchunks + TM_G - 1) / TM_G) + 2 * (NB + 1) + 4);
+}
+
 size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
   int SH = 0;
   uint32_t NB = 0;
@@ -505,7 +519,8 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
   if (SH_out) *SH_out = SH;
   if (NB_out) *NB_out = NB;
   uint64_t cw = (uint64_t)NB * nchunks;
-  return 2 * cw + scan_tmp_words(cw) + (2 * m + 1) / 2 + 16;  // counts, offsets, scan tmp, u16 ep (+pad)
+  // counts, offsets, scan tmp (flat scan, or group sums + bucket starts), u16 ep (+pad)
+  return 2 * cw + degb_scan_words(cw, nchunks, NB) + (2 * m + 1) / 2 + 16;
 }
 
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
@@ -530,22 +545,33 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   uint32_t* counts = tmp;
   uint32_t* offsets = tmp + cw;
   uint32_t* stmp = offsets + cw;
-  uint16_t* ep = (uint16_t*)(((uintptr_t)(stmp + scan_tmp_words(cw)) + 15) & ~(uintptr_t)15);
+  uint16_t* ep = (uint16_t*)(((uintptr_t)(stmp + degb_scan_words(cw, nchunks, NB)) + 15) & ~(uintptr_t)15);
   uint32_t H = SH > 15 ? 2u : 1u;
+  // tile-major counts (SHEEP_BIN_TM, as the hi bins): bucket starts come from the scan
+  const int tm = bin_tile_major() ? 1 : 0;
+  unsigned long long* bstart = nullptr;
   hipLaunchKernelGGL(k_degb_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
-                     n_ids, file_mode, SH, NB, counts, nchunks, err, psh, yhist);
-  launch_scan_exclusive(counts, offsets, cw, stmp, s);
+                     n_ids, file_mode, SH, NB, counts, nchunks, err, psh, yhist, tm);
+  if (tm) {
+    uint32_t* gsum = stmp;
+    bstart = (unsigned long long*)(((uintptr_t)(gsum + NB * ((nchunks + TM_G - 1) / TM_G)) + 7) &
+                                   ~(uintptr_t)7);
+    tm_offsets(counts, offsets, nchunks, NB, NB, gsum, bstart, s);
+  } else {
+    launch_scan_exclusive(counts, offsets, cw, stmp, s);
+  }
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
-                     nchunks, ep, selfc);
+                     nchunks, ep, selfc, tm);
   const char* eh = getenv("SHEEP_DEGB_HIST");
   if (H > 1 && !(eh && atoi(eh) == 0))
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
-                       (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg);
+                       (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
+                       (const unsigned long long*)bstart);
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
-                       deg);
+                       deg, (const unsigned long long*)bstart);
   return yhist != nullptr;
 }
 
@@ -720,62 +746,83 @@ __global__ void k_bin_starts(const uint32_t* __restrict__ offsets, uint32_t ntil
 //   k_tm_rows         counts[t][bin] <- bin_start[bin] + gsum[g][bin] + earlier tiles of g.
 // The digit-major layout had every tile write (edge pass) and read (scatter) 512 words that
 // lie ntiles words apart: 131 K tiles x 512 x a 64-B sector each way at RMAT-26.
-static constexpr uint32_t TM_G = 256;  // tiles per group
+// NC columns (bins) per tile row; launched with blockDim.x >= NC (threads beyond NC idle).
 
-__global__ void __launch_bounds__(512)
-k_tm_colsum(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ gsum) {
+__global__ void __launch_bounds__(1024)
+k_tm_colsum(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t NC,
+            uint32_t* __restrict__ gsum) {
   const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
+  if (d >= NC) return;
   uint32_t sum = 0;
   for (uint32_t t = t0; t < t1; t += 8) {
     uint32_t v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? counts[(uint64_t)(t + u) * 512 + d] : 0u;
+    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? counts[(uint64_t)(t + u) * NC + d] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u) sum += v[u];
   }
-  gsum[(uint64_t)blockIdx.x * 512 + d] = sum;
+  gsum[(uint64_t)blockIdx.x * NC + d] = sum;
 }
 
-__global__ void __launch_bounds__(512)
-k_tm_scan_groups(uint32_t* __restrict__ gsum, uint32_t ngroups, uint32_t nb, uint64_t n,
+// One block.  bin_start[d] (d < nb) = exclusive prefix of the column totals; bin_start[nb] =
+// the grand total (columns nb..NC-1 must be empty).
+__global__ void __launch_bounds__(1024)
+k_tm_scan_groups(uint32_t* __restrict__ gsum, uint32_t ngroups, uint32_t NC, uint32_t nb,
                  unsigned long long* __restrict__ bin_start) {
-  __shared__ uint32_t wsum[8];
+  __shared__ uint32_t wsum[16];
   const uint32_t d = threadIdx.x, lane = d & 63, w = d >> 6;
   uint32_t run = 0;
-  for (uint32_t g = 0; g < ngroups; g += 8) {
-    uint32_t v[8];
+  if (d < NC)
+    for (uint32_t g = 0; g < ngroups; g += 8) {
+      uint32_t v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = g + u < ngroups ? gsum[(uint64_t)(g + u) * 512 + d] : 0u;
+      for (int u = 0; u < 8; ++u) v[u] = g + u < ngroups ? gsum[(uint64_t)(g + u) * NC + d] : 0u;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (g + u < ngroups) gsum[(uint64_t)(g + u) * 512 + d] = run;
-      run += v[u];
+      for (int u = 0; u < 8; ++u) {
+        if (g + u < ngroups) gsum[(uint64_t)(g + u) * NC + d] = run;
+        run += v[u];
+      }
     }
-  }
   const uint32_t incl = wave_incl_scan(run);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   uint32_t add = 0;
   for (uint32_t i = 0; i < w; ++i) add += wsum[i];
   if (d < nb) bin_start[d] = add + incl - run;
-  if (d == 0) bin_start[nb] = n;
+  if (d == blockDim.x - 1) bin_start[nb] = add + incl;
 }
 
-__global__ void __launch_bounds__(512)
-k_tm_rows(uint32_t* __restrict__ counts, uint32_t ntiles, const uint32_t* __restrict__ gsum,
-          const unsigned long long* __restrict__ bin_start, uint32_t nb) {
+// out[t][d] = bin_start[d] + gsum[g][d] + in[t'][d] summed over the earlier tiles t' of g
+// (out may alias in).
+__global__ void __launch_bounds__(1024)
+k_tm_rows(const uint32_t* in, uint32_t* out, uint32_t ntiles, uint32_t NC,
+          const uint32_t* __restrict__ gsum, const unsigned long long* __restrict__ bin_start,
+          uint32_t nb) {
   const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
-  uint32_t run = (d < nb ? (uint32_t)bin_start[d] : 0u) + gsum[(uint64_t)blockIdx.x * 512 + d];
+  if (d >= NC) return;
+  uint32_t run = (d < nb ? (uint32_t)bin_start[d] : 0u) + gsum[(uint64_t)blockIdx.x * NC + d];
   for (uint32_t t = t0; t < t1; t += 8) {
     uint32_t v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? counts[(uint64_t)(t + u) * 512 + d] : 0u;
+    for (int u = 0; u < 8; ++u) v[u] = t + u < t1 ? in[(uint64_t)(t + u) * NC + d] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (t + u < t1) counts[(uint64_t)(t + u) * 512 + d] = run;
+      if (t + u < t1) out[(uint64_t)(t + u) * NC + d] = run;
       run += v[u];
     }
   }
+}
+
+// Tile-major exclusive offsets of an ntiles x NC count matrix (gsum: NC * ceil(ntiles / TM_G)
+// words of scratch); bin_start: nb + 1 u64 (column starts, then the total).
+static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
+                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s) {
+  const uint32_t ng = (ntiles + TM_G - 1) / TM_G;
+  const unsigned th = NC <= 512 ? 512 : 1024;
+  hipLaunchKernelGGL(k_tm_colsum, dim3(ng), dim3(th), 0, s, counts, ntiles, NC, gsum);
+  hipLaunchKernelGGL(k_tm_scan_groups, dim3(1), dim3(th), 0, s, gsum, ng, NC, nb, bin_start);
+  hipLaunchKernelGGL(k_tm_rows, dim3(ng), dim3(th), 0, s, counts, offsets, ntiles, NC,
+                     (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb);
 }
 
 // SHEEP_BIN_TM=0: the digit-major counts and one flat scan (the previous layout).
@@ -790,14 +837,8 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   if (bin_tile_major()) {
-    const uint32_t ng = (uint32_t)((nt + TM_G - 1) / TM_G);
-    uint32_t* gsum = tmp + 512 * nt;
     if (n == 0) return;
-    hipLaunchKernelGGL(k_tm_colsum, dim3(ng), dim3(512), 0, s, (const uint32_t*)counts, (uint32_t)nt,
-                       gsum);
-    hipLaunchKernelGGL(k_tm_scan_groups, dim3(1), dim3(512), 0, s, gsum, ng, nb, n, bin_start);
-    hipLaunchKernelGGL(k_tm_rows, dim3(ng), dim3(512), 0, s, counts, (uint32_t)nt,
-                       (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb);
+    tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
     hipLaunchKernelGGL((k_rsort_scatter<9, true, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in,
                        out, n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
     return;
