@@ -615,7 +615,7 @@ __device__ __forceinline__ uint64_t digit_match(uint32_t d, bool valid) {
   return match;
 }
 
-template <int DB>  // digit bits: 8 or 9
+template <int DB, bool TM = false>  // digit bits: 8 or 9; TM: tile-major counts
 __global__ void __launch_bounds__(RS_THREADS)
 k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* __restrict__ counts,
               uint32_t ntiles) {
@@ -641,7 +641,7 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
   }
   __syncthreads();
   for (uint32_t i = t; i < NBIN; i += RS_THREADS)
-    counts[(uint64_t)i * ntiles + blockIdx.x] = hist[i];
+    counts[TM ? (uint64_t)blockIdx.x * NBIN + i : (uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
 
 // TM: offsets are tile-major (offsets[tile * NBIN + digit], see k_tm_rows) instead of
@@ -854,7 +854,8 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
 
 size_t rsort_tmp_words(uint64_t n) {
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
-  return 512 * nt + std::max<size_t>(scan_tmp_words(512 * nt), 512 * ((nt + TM_G - 1) / TM_G));
+  // counts; then the flat scan's tmp, or the group sums + 513 u64 column starts (tile-major)
+  return 512 * nt + std::max<size_t>(scan_tmp_words(512 * nt), 512 * ((nt + TM_G - 1) / TM_G) + 1030);
 }
 
 // Digit width of the first pass when `bits` are sorted in passes of <= 9 bits (even split,
@@ -873,28 +874,34 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   uint32_t* stmp = tmp + 512 * nt;
+  const bool tm = bin_tile_major();  // counted0: launch_edge_pass_tiles used the same layout
+  unsigned long long* dstart =
+      (unsigned long long*)(((uintptr_t)(stmp + 512 * ((nt + TM_G - 1) / TM_G)) + 7) & ~(uintptr_t)7);
   const uint64_t* src = in;
   uint64_t* dst = a;
   for (int shift = bit_lo, p = 0; shift < bit_hi; ++p) {
     int width = rsort_first_width(bit_hi - shift);
     if (n) {
       bool count = !(p == 0 && counted0);
+      const dim3 g((unsigned)nt), bl(RS_THREADS);
       if (width > 8) {
         if (count)
-          hipLaunchKernelGGL(k_rsort_count<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+          hipLaunchKernelGGL((tm ? k_rsort_count<9, true> : k_rsort_count<9, false>), g, bl, 0, s, src, n,
                              shift, counts, (uint32_t)nt);
-        launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
-        hipLaunchKernelGGL(k_rsort_scatter<9>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
-                           (const uint16_t*)nullptr);
+        if (tm) tm_offsets(counts, counts, (uint32_t)nt, 512, 512, stmp, dstart, s);
+        else launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
+        hipLaunchKernelGGL((tm ? k_rsort_scatter<9, false, true> : k_rsort_scatter<9, false, false>), g, bl,
+                           0, s, src, dst, n, shift, (const uint32_t*)counts, (uint32_t)nt,
+                           (const uint32_t*)nullptr, 0u, (const uint16_t*)nullptr);
       } else {
         if (count)
-          hipLaunchKernelGGL(k_rsort_count<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, n,
+          hipLaunchKernelGGL((tm ? k_rsort_count<8, true> : k_rsort_count<8, false>), g, bl, 0, s, src, n,
                              shift, counts, (uint32_t)nt);
-        launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
-        hipLaunchKernelGGL(k_rsort_scatter<8>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, src, dst,
-                           n, shift, (const uint32_t*)counts, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
-                           (const uint16_t*)nullptr);
+        if (tm) tm_offsets(counts, counts, (uint32_t)nt, 256, 256, stmp, dstart, s);
+        else launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
+        hipLaunchKernelGGL((tm ? k_rsort_scatter<8, false, true> : k_rsort_scatter<8, false, false>), g, bl,
+                           0, s, src, dst, n, shift, (const uint32_t*)counts, (uint32_t)nt,
+                           (const uint32_t*)nullptr, 0u, (const uint16_t*)nullptr);
       }
     }
     shift += width;
@@ -1115,8 +1122,11 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
                             uint32_t* tmp, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
-  auto k = DB > 8 ? (pre ? k_edge_pass_tiles<9, true> : k_edge_pass_tiles<9, false>)
-                  : (pre ? k_edge_pass_tiles<8, true> : k_edge_pass_tiles<8, false>);
+  const bool tm = bin_tile_major();  // the layout radix_sort_u64(..., counted0) expects
+  auto k = DB > 8 ? (pre ? (tm ? k_edge_pass_tiles<9, true, false, true> : k_edge_pass_tiles<9, true>)
+                         : (tm ? k_edge_pass_tiles<9, false, false, true> : k_edge_pass_tiles<9, false>))
+                  : (pre ? (tm ? k_edge_pass_tiles<8, true, false, true> : k_edge_pass_tiles<8, true>)
+                         : (tm ? k_edge_pass_tiles<8, false, false, true> : k_edge_pass_tiles<8, false>));
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
                      pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
                      (uint16_t*)nullptr);
