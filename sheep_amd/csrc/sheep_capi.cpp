@@ -238,10 +238,12 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 
 // kb bucket counts: each bucket costs a fixed ~60-100 us of launches and small kernels, while
 // too few buckets leave the zipper long in-bucket walks (profiles/r01/kb_bucket_sweep.txt).
-// kmax: 64 for the one-GPU loop (its map, on the critical path, wants short buckets); the
-// lockstep loop's critical path is the apply, whose per-bucket cost favours fewer buckets
-// (RMAT-26, P = 8 simulation: K = 40/48/56/64 -> apply 18.8/18.7/19.2/20.5 ms).
-static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 64) {
+// kmax: 48 for the one-GPU loop (RMAT-26, K_e = K_r = 32/40/48/64/80 -> 81.6/71.9/71.9/74.4/
+// 76.1 ms, profiles/r01/kb_bucket_sweep_r01b.txt: below ~40 a bucket's in-bucket walks grow
+// long, above it the fixed per-bucket cost dominates); 40 for the lockstep loop, whose
+// critical path is the apply (RMAT-26, P = 8 simulation: K = 40/48/56/64 -> apply
+// 18.8/18.7/19.2/20.5 ms).
+static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 48) {
   const char* ek = getenv("SHEEP_KB_BUCKETS");
   const char* er = getenv("SHEEP_KB_RANKB");
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
@@ -407,7 +409,7 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 // The cuts as bin indices (sorted, distinct, in (0, nb - 1)).
 static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                                          const std::vector<unsigned long long>& bin_start,
-                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 64) {
+                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 48) {
   const uint32_t nb = (uint32_t)bounds.size();
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
