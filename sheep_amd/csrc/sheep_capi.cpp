@@ -81,6 +81,7 @@ static Ctx& init_ctx(int device) {
     HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     for (auto& e : c.kb_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : c.part_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&c.d_err, 16));
     HIP_CHECK(hipMemset(c.d_err, 0, 16));
     HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
@@ -207,7 +208,15 @@ struct DegInfo {
   const uint32_t* selfc = nullptr;  // self-loop records per vid
   int mode = SHEEP_DEGREE_LLAMA;
   bool yhist_ready = false;         // degree_dev counted the partition's y digits (part_ws)
+  bool part_first_done = false;     // the first partition pass was launched on c.side into
+                                    // e_items; c.part_ev[1] marks its end
 };
+
+// Rank gathers in partitioned order (launch_part_gather) for large inputs.
+static bool use_part(uint64_t m) {
+  const char* ep = getenv("SHEEP_EDGE_PART");
+  return ep ? atoi(ep) != 0 : m >= (1ull << 22);
+}
 
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
                              uint32_t* d_rank, hipStream_t s) {
@@ -493,12 +502,16 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
   bool pst_count = kb && di;
   // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
-  const char* ep = getenv("SHEEP_EDGE_PART");
-  bool part = ep ? atoi(ep) != 0 : m >= (1ull << 22);
+  bool part = use_part(m);
   const uint32_t* src = d_uv;
   if (part) {
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
-    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready);
+    if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
+      HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
+    } else {
+      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready);
+    }
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
   }
@@ -1001,15 +1014,29 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
   const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true);
   tm.mark("degree");
+  // The first partition pass of the rank gathers needs no ranks: it runs on the side stream
+  // while the sequence is sorted (SHEEP_PART_OVERLAP=0: in line, after it).
+  static const char* epo = getenv("SHEEP_PART_OVERLAP");
+  const bool overlap = (epo ? atoi(epo) != 0 : true) && m > 0 && use_part(m);
+  if (overlap) {
+    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    HIP_CHECK(hipEventRecord(c.part_ev[0], s));
+    HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
+    HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
+  }
   uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
   tm.mark("sequence");
   DegInfo di;
+  di.part_first_done = overlap;
   di.yhist_ready = yh;
   di.seq = d_seq;
   di.deg = deg;
   di.selfc = selfc;
   di.mode = degree_mode;
   build_tree_dev(c, d_uv, m, rank, n_ids, n_seq, d_parent, d_pst, s, &tm, &di);
+  if (overlap) HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));  // also when no tree was built
   check_err(c, s);
   tm.finish(c);
   if (n_seq_out) *n_seq_out = n_seq;

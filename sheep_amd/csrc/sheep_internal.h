@@ -31,6 +31,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;     // second stream of the pipelined kb loop
   hipEvent_t kb_ev[5] = {};       // kb loop: [0,1] map done, [2,3] apply done (by parity), [4] start
+  hipEvent_t part_ev[2] = {};     // graph2tree: [0] degree done, [1] first partition pass done
   Scratch scratch;
   uint32_t* d_err = nullptr;     // device error word
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
@@ -95,6 +96,12 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
                         bool yhist_ready = false);
+// The two passes of launch_part_gather separately (the first needs no ranks, so it can run
+// while the sequence is sorted): uv -> mid (y-digit order), then mid -> pre (x-digit order).
+void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
+                       uint32_t* ws, hipStream_t s, bool yhist_ready);
+void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* pre, uint32_t* ws, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
                            hipStream_t s);

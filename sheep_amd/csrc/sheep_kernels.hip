@@ -1252,13 +1252,16 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
 }
 
 // uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: 512 u32 + 256 u64.
-void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
-                        bool yhist_ready) {
-  if (m == 0) return;
+static int part_shift(uint32_t n_rank) {
   int bits = 0;
   for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
-  int sh = bits > 8 ? bits - 8 : 0;
+  return bits > 8 ? bits - 8 : 0;
+}
+
+void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
+                       uint32_t* ws, hipStream_t s, bool yhist_ready) {
+  if (m == 0) return;
+  const int sh = part_shift(n_rank);
   uint32_t* yhist = ws;
   uint32_t* xhist = ws + 256;
   unsigned long long* cursor = (unsigned long long*)(ws + 512);
@@ -1271,10 +1274,26 @@ void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, ui
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
   uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
   hipLaunchKernelGGL(k_part<0>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)uv, m,
-                     mid, cursor, xhist, sh, rank, n_rank);
+                     mid, cursor, xhist, sh, (const uint32_t*)nullptr, n_rank);
+}
+
+void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* pre, uint32_t* ws, hipStream_t s) {
+  if (m == 0) return;
+  const int sh = part_shift(n_rank);
+  uint32_t* xhist = ws + 256;
+  unsigned long long* cursor = (unsigned long long*)(ws + 512);
+  uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, xhist, cursor);
-  hipLaunchKernelGGL(k_part<1>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)mid, m,
+  hipLaunchKernelGGL(k_part<1>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, mid, m,
                      pre, cursor, xhist, sh, rank, n_rank);
+}
+
+void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
+                        bool yhist_ready) {
+  launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready);
+  launch_part_second(mid, m, rank, n_rank, pre, ws, s);
 }
 
 // ---------------------------------------------------------------------------------------
