@@ -189,7 +189,8 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 // Returns true when the bucketed path also counted the rank-gather partition's y digits into
 // the "part_ws" scratch (yhist).
 static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
-                       uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s, bool want_yhist = false) {
+                       uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s, bool want_yhist = false,
+                       hipEvent_t counted = nullptr) {
   const char* e = getenv("SHEEP_DEGREE");
   bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
   if (!bucketed || n_ids == 0) {
@@ -198,7 +199,8 @@ static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
   }
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
   uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
-  return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist);
+  return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist,
+                                counted);
 }
 
 // Optional degree information for pst without per-edge atomics (launch_pst_from_degree).
@@ -1012,16 +1014,21 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* selfc = (uint32_t*)c.scratch.get("selfc", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
-  const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true);
-  tm.mark("degree");
-  // The first partition pass of the rank gathers needs no ranks: it runs on the side stream
-  // while the sequence is sorted (SHEEP_PART_OVERLAP=0: in line, after it).
+  // The first partition pass of the rank gathers needs no ranks, only the y-digit counts of
+  // the degree pass's first kernel: it runs on the side stream beside the rest of the degree
+  // pass and the sequence sort (SHEEP_PART_OVERLAP=0: in line, after them; =1: after the
+  // whole degree pass).
   static const char* epo = getenv("SHEEP_PART_OVERLAP");
-  const bool overlap = (epo ? atoi(epo) != 0 : true) && m > 0 && use_part(m);
+  const int ov = epo ? atoi(epo) : 2;
+  const bool overlap = ov != 0 && m > 0 && use_part(m);
+  if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
+  const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
+                             overlap && ov == 2 ? c.part_ev[0] : nullptr);
+  tm.mark("degree");
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
-    HIP_CHECK(hipEventRecord(c.part_ev[0], s));
+    if (ov != 2) HIP_CHECK(hipEventRecord(c.part_ev[0], s));
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));

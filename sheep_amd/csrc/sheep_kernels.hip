@@ -526,7 +526,7 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
-                            hipStream_t s, uint32_t* yhist) {
+                            hipStream_t s, uint32_t* yhist, hipEvent_t counted) {
   int SH;
   uint32_t NB;
   if (!degb_params(n_ids, &SH, &NB)) {
@@ -552,6 +552,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   unsigned long long* bstart = nullptr;
   hipLaunchKernelGGL(k_degb_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, counts, nchunks, err, psh, yhist, tm);
+  if (counted) (void)hipEventRecord(counted, s);
   if (tm) {
     uint32_t* gsum = stmp;
     bstart = (unsigned long long*)(((uintptr_t)(gsum + NB * ((nchunks + TM_G - 1) / TM_G)) + 7) &
