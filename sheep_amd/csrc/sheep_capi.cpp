@@ -190,17 +190,18 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 // the "part_ws" scratch (yhist).
 static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
                        uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s, bool want_yhist = false,
-                       hipEvent_t counted = nullptr) {
+                       hipEvent_t counted = nullptr, uint32_t* stats = nullptr) {
   const char* e = getenv("SHEEP_DEGREE");
   bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
   if (!bucketed || n_ids == 0) {
     launch_degree(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, s);
+    if (stats) launch_deg_stats(d_deg, n_ids, stats, s);
     return false;
   }
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
   uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
   return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist,
-                                counted);
+                                counted, stats);
 }
 
 // Optional degree information for pst without per-edge atomics (launch_pst_from_degree).
@@ -220,11 +221,12 @@ static bool use_part(uint64_t m) {
   return ep ? atoi(ep) != 0 : m >= (1ull << 22);
 }
 
+// stats_ready: the degree pass already wrote max degree / zero-degree count to "stats".
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
-                             uint32_t* d_rank, hipStream_t s) {
+                             uint32_t* d_rank, hipStream_t s, bool stats_ready = false) {
   if (n_ids == 0) return 0;
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
-  launch_deg_stats(d_deg, n_ids, stats, s);
+  if (!stats_ready) launch_deg_stats(d_deg, n_ids, stats, s);
   HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   uint32_t maxdeg = c.h_pinned[0], zeros = c.h_pinned[1];
@@ -1022,8 +1024,9 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   const int ov = epo ? atoi(epo) : 2;
   const bool overlap = ov != 0 && m > 0 && use_part(m);
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
+  uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
   const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
-                             overlap && ov == 2 ? c.part_ev[0] : nullptr);
+                             overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
   tm.mark("degree");
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
@@ -1033,7 +1036,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
-  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true);
   tm.mark("sequence");
   DegInfo di;
   di.part_first_done = overlap;

@@ -56,7 +56,8 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                             hipStream_t s, uint32_t* yhist = nullptr,
-                            hipEvent_t counted = nullptr /* recorded once yhist is complete */);
+                            hipEvent_t counted = nullptr /* recorded once yhist is complete */,
+                            uint32_t* stats = nullptr /* [0] max degree, [1] zero-degree ids */);
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max,[1]=zeros*/,
                       hipStream_t s);
 // Exclusive scan of n u32 (n < 2^32); tmp needs scan_tmp_words(n) u32.

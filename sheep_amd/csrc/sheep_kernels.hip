@@ -265,6 +265,22 @@ void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32
 // Supports n_ids <= 2^26 (launch_degree_bucketed falls back to k_degree above that).
 // ---------------------------------------------------------------------------------------
 static constexpr int DEGB_THREADS = 1024;
+// k_deg_stats folded into the histogram kernels: the block's max degree and zero-degree ids,
+// two global atomics per block (called by every thread of a DEGB_THREADS block).
+__device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, uint32_t zeros) {
+  __shared__ uint32_t smx[DEGB_THREADS / 64], szr[DEGB_THREADS / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    zeros += (uint32_t)__shfl_xor((int)zeros, o);
+  }
+  if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = mx; szr[threadIdx.x >> 6] = zeros; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < DEGB_THREADS / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; }
+    if (mx) atomicMax(&stats[0], mx);
+    if (zeros) atomicAdd(&stats[1], zeros);
+  }
+}
 // Tile-major count matrices and their scan (defined with the hi bins below).
 static bool bin_tile_major();
 static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
@@ -372,7 +388,8 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
-            uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart) {
+            uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
+            uint32_t* __restrict__ stats) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
@@ -421,8 +438,15 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
   }
   __syncthreads();
   uint64_t g0 = ((uint64_t)b << SH) + (uint64_t)h * span;
+  uint32_t mx = 0, zeros = 0;
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x)
-    if (g0 + i < n_ids) deg[g0 + i] = cnt[i];
+    if (g0 + i < n_ids) {
+      const uint32_t d = cnt[i];
+      deg[g0 + i] = d;
+      mx = max(mx, d);
+      zeros += d == 0;
+    }
+  if (stats) deg_stats_flush(stats, mx, zeros);
 }
 
 // Buckets of 65536 ids (n_ids > 2^25): one workgroup per bucket reads the bucket's run ONCE
@@ -433,7 +457,8 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
               const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, uint32_t n_ids,
-              uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart) {
+              uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
+              uint32_t* __restrict__ stats) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -488,11 +513,17 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
     __syncthreads();
   }
   const uint64_t base = (uint64_t)b << 16;
+  uint32_t mx = 0, zeros = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     const uint64_t id = base + (uint64_t)k * DEGB_THREADS + threadIdx.x;
-    if (id < n_ids) deg[id] = acc[k];
+    if (id < n_ids) {
+      deg[id] = acc[k];
+      mx = max(mx, acc[k]);
+      zeros += acc[k] == 0;
+    }
   }
+  if (stats) deg_stats_flush(stats, mx, zeros);
 }
 
 // SH: local-id bits, NB buckets; false when n_ids is beyond the bucketed path (> 2^26).
@@ -526,20 +557,29 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
-                            hipStream_t s, uint32_t* yhist, hipEvent_t counted) {
+                            hipStream_t s, uint32_t* yhist, hipEvent_t counted, uint32_t* stats) {
   int SH;
   uint32_t NB;
   if (!degb_params(n_ids, &SH, &NB)) {
     launch_degree(uv, m, n_ids, file_mode, deg, selfc, err, s);
+    if (stats) launch_deg_stats(deg, n_ids, stats, s);
     return false;
   }
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
-  if (n_ids == 0) return false;
-  if (m == 0) { (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s); return false; }
+  if (n_ids == 0) {
+    if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+    return false;
+  }
+  if (m == 0) {
+    (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
+    if (stats) launch_deg_stats(deg, n_ids, stats, s);
+    return false;
+  }
   int pbits = 0;
   for (uint32_t v = n_ids - 1; v; v >>= 1) ++pbits;
   const int psh = pbits > 8 ? pbits - 8 : 0;  // as launch_part_gather with n_rank = n_ids
   if (yhist) (void)hipMemsetAsync(yhist, 0, 256 * 4, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
   uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   uint64_t cw = (uint64_t)NB * nchunks;
   uint32_t* counts = tmp;
@@ -568,11 +608,11 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   if (H > 1 && !(eh && atoi(eh) == 0))
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
-                       (const unsigned long long*)bstart);
+                       (const unsigned long long*)bstart, stats);
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
-                       deg, (const unsigned long long*)bstart);
+                       deg, (const unsigned long long*)bstart, stats);
   return yhist != nullptr;
 }
 
