@@ -211,6 +211,7 @@ struct DegInfo {
   const uint32_t* selfc = nullptr;  // self-loop records per vid
   int mode = SHEEP_DEGREE_LLAMA;
   bool yhist_ready = false;         // degree_dev counted the partition's y digits (part_ws)
+  const uint32_t* nsd = nullptr;    // rank-ordered deg - w * selfc (nullable, see sequence_dev)
   bool part_first_done = false;     // the first partition pass was launched on c.side into
                                     // e_items; c.part_ev[1] marks its end
 };
@@ -222,8 +223,12 @@ static bool use_part(uint64_t m) {
 }
 
 // stats_ready: the degree pass already wrote max degree / zero-degree count to "stats".
+// nsd (nullable, n_ids words): rank-ordered non-self-loop degrees (k_unpack_seq) for these
+// same records' selfc / mode.
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
-                             uint32_t* d_rank, hipStream_t s, bool stats_ready = false) {
+                             uint32_t* d_rank, hipStream_t s, bool stats_ready = false,
+                             uint32_t* nsd = nullptr, const uint32_t* selfc = nullptr,
+                             int mode = 0) {
   if (n_ids == 0) return 0;
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
   if (!stats_ready) launch_deg_stats(d_deg, n_ids, stats, s);
@@ -239,7 +244,7 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
   launch_pack_deg(d_deg, n_ids, items, s);
   uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
-  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s);
+  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
   return n_seq;
 }
 
@@ -531,7 +536,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   if (use_bins) {
     const size_t nch = ((size_t)n_seq + 255) / 256;
     uint64_t* cds = (uint64_t*)c.scratch.get("chunk_deg", nch * 8);
-    launch_chunk_degsum(di->seq, di->deg, n_seq, cds, s);
+    launch_chunk_degsum(di->seq, di->deg, n_seq, cds, s, di->nsd);
     std::vector<uint64_t> hd(nch);
     HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -569,7 +574,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
                    use_bins ? &given : nullptr, dbins, nbins);
   if (tm) tm->mark("tree_insert");
   if (pst_count) {
-    launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s);
+    launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s, di->nsd);
     if (tm) tm->mark("pst");
   }
   if (stats) {
@@ -1036,9 +1041,11 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
-  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true);
+  uint32_t* nsd = (uint32_t*)c.scratch.get("nsd", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true, nsd, selfc, degree_mode);
   tm.mark("sequence");
   DegInfo di;
+  di.nsd = nsd;
   di.part_first_done = overlap;
   di.yhist_ready = yh;
   di.seq = d_seq;

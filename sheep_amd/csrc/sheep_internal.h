@@ -70,7 +70,8 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
                          int bit_hi, uint32_t* tmp, hipStream_t s, bool counted0 = false);
 void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s);
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
-                       uint32_t* rank, hipStream_t s);
+                       uint32_t* rank, hipStream_t s, uint32_t* nsd = nullptr,
+                       const uint32_t* selfc = nullptr, int file_mode = 0);
 void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s);
 void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
                          hipStream_t s);
@@ -85,7 +86,7 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
 // the edge pass counting bins (no pst; nb <= 512 bounds, bounds[0] = 0, bounds[nb-1] = n_seq
 // so that INVALID his fall in the last bin), and the scatter by bin (bin_start: nb+1 u64).
 void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_seq, uint64_t* out,
-                         hipStream_t s);
+                         hipStream_t s, const uint32_t* nsd = nullptr);
 // digits: m u16 scratch (each item's bin, written by the edge pass, read by the scatter)
 void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                            uint64_t* items, uint32_t* err, const uint32_t* bins, uint32_t nb,
@@ -106,7 +107,8 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
                         uint64_t* pre, uint32_t* ws, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
-                           hipStream_t s);
+                           hipStream_t s,
+                           const uint32_t* nsd = nullptr);
 // variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
 void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
                         int variant, bool stats, unsigned long long* ws, hipStream_t s);

@@ -92,21 +92,27 @@ __global__ void k_pst_from_degree(const uint32_t* __restrict__ seq, uint32_t n_s
 }
 
 // pst[r] = nsdeg[seq[r]] - cnt[r], cnt[r] = |{records with hi == r}| (counted by k_kb_map).
+// nsd (nullable): nsdeg already in rank order (k_unpack_seq), read instead of two gathers.
 __global__ void k_pst_from_count(const uint32_t* __restrict__ seq, uint32_t n_seq,
                                  const uint32_t* __restrict__ deg, const uint32_t* __restrict__ selfc,
-                                 uint32_t w, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ pst) {
+                                 uint32_t w, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ pst,
+                                 const uint32_t* __restrict__ nsd) {
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_seq; r += gridDim.x * blockDim.x) {
-    uint32_t v = seq[r];
-    pst[r] = deg[v] - w * selfc[v] - cnt[r];
+    if (nsd) {
+      pst[r] = nsd[r] - cnt[r];
+    } else {
+      uint32_t v = seq[r];
+      pst[r] = deg[v] - w * selfc[v] - cnt[r];
+    }
   }
 }
 
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
-                           hipStream_t s) {
+                           hipStream_t s, const uint32_t* nsd) {
   if (n_seq == 0) return;
   hipLaunchKernelGGL(k_pst_from_count, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, seq, n_seq, deg,
-                     selfc, file_mode ? 2u : 1u, cnt, pst);
+                     selfc, file_mode ? 2u : 1u, cnt, pst, nsd);
 }
 
 void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* seq, uint32_t n_seq,
@@ -959,12 +965,18 @@ __global__ void k_pack_deg(const uint32_t* __restrict__ deg, uint32_t n, uint64_
     items[i] = ((uint64_t)deg[i] << 32) | i;
 }
 
+// nsd (nullable): nsd[i] = degree - w * self-loop records of seq[i] (the non-self-loop
+// degree that pst needs), in rank order; the degree is the sorted item's key.
 __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros, uint32_t n_seq,
-                             uint32_t* __restrict__ seq, uint32_t* __restrict__ rank) {
+                             uint32_t* __restrict__ seq, uint32_t* __restrict__ rank,
+                             uint32_t* __restrict__ nsd, const uint32_t* __restrict__ selfc,
+                             uint32_t w) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_seq; i += gridDim.x * blockDim.x) {
-    uint32_t v = (uint32_t)items[zeros + i];
+    const uint64_t it = items[zeros + i];
+    uint32_t v = (uint32_t)it;
     seq[i] = v;
     if (rank) rank[v] = i;
+    if (nsd) nsd[i] = (uint32_t)(it >> 32) - w * selfc[v];
   }
 }
 
@@ -973,10 +985,11 @@ void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream
 }
 
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
-                       uint32_t* rank, hipStream_t s) {
+                       uint32_t* rank, hipStream_t s, uint32_t* nsd, const uint32_t* selfc,
+                       int file_mode) {
   if (n_seq)
     hipLaunchKernelGGL(k_unpack_seq, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, items, zeros, n_seq,
-                       seq, rank);
+                       seq, rank, nsd, selfc, file_mode ? 2u : 1u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1044,8 +1057,11 @@ void launch_edge_pass(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint
 // The estimate only shapes the work; any bins give the same tree.
 // ---------------------------------------------------------------------------------------
 // out[c] = sum of deg[seq[r]] over r in [256 c, 256 c + 256) (one wave per chunk).
+// nsd (nullable): rank-ordered degrees (k_unpack_seq's non-self-loop degrees: the bins are only
+// an estimate) read instead of gathering deg[seq[r]].
 __global__ void k_chunk_degsum(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ deg,
-                               uint32_t n_seq, uint64_t* __restrict__ out) {
+                               uint32_t n_seq, uint64_t* __restrict__ out,
+                               const uint32_t* __restrict__ nsd) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nch = (n_seq + 255) / 256;
   for (uint32_t ch = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; ch < nch;
@@ -1054,7 +1070,7 @@ __global__ void k_chunk_degsum(const uint32_t* __restrict__ seq, const uint32_t*
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       uint32_t r = ch * 256 + k * 64 + lane;
-      if (r < n_seq) sum += deg[seq[r]];
+      if (r < n_seq) sum += nsd ? nsd[r] : deg[seq[r]];
     }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o);
     if (lane == 0) out[ch] = sum;
@@ -1062,9 +1078,9 @@ __global__ void k_chunk_degsum(const uint32_t* __restrict__ seq, const uint32_t*
 }
 
 void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_seq, uint64_t* out,
-                         hipStream_t s) {
+                         hipStream_t s, const uint32_t* nsd) {
   if (n_seq) hipLaunchKernelGGL(k_chunk_degsum, dim3(grid_for((uint64_t)(n_seq + 255) / 256 * 64)),
-                                dim3(BLOCK), 0, s, seq, deg, n_seq, out);
+                                dim3(BLOCK), 0, s, seq, deg, n_seq, out, nsd);
 }
 
 
