@@ -872,6 +872,64 @@ static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntile
                      (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb);
 }
 
+// The hi-bin scatter without stability (the order inside a bin is free: the kb loop and pst
+// never depend on it): 16384-item tiles — two of the edge pass's 8192-item count tiles, whose
+// runs of a bin are adjacent in the output, so the tile's base for bin d is the first one's
+// tile-major offset — ranked by LDS atomics, staged in bin order, and written as whole runs
+// per wave (runs twice as long as the stable scatter's, without its 9-ballot rank).
+static constexpr int BS_TILE = 2 * RS_TILE;
+
+__global__ void __launch_bounds__(1024)
+k_bin_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n,
+              const uint32_t* __restrict__ offsets, const uint16_t* __restrict__ digits) {
+  constexpr int NT = 1024, IT = BS_TILE / NT;
+  __shared__ uint64_t stage[BS_TILE];
+  __shared__ uint32_t hist[512], tstart[512], goff[512], wsum[NT / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * BS_TILE;
+  const uint32_t tile_n = (uint32_t)min((uint64_t)BS_TILE, n - tbase);
+  if (t < 512) {
+    hist[t] = 0;
+    goff[t] = offsets[(uint64_t)(2 * blockIdx.x) * 512 + t];
+  }
+  uint64_t it[IT];
+  uint32_t dg[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const uint32_t j = (uint32_t)k * NT + t;
+    it[k] = j < tile_n ? in[tbase + j] : 0ull;
+    dg[k] = j < tile_n ? digits[tbase + j] : 0u;
+  }
+  __syncthreads();
+  uint32_t li[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k)
+    if ((uint32_t)k * NT + t < tile_n) li[k] = atomicAdd(&hist[dg[k]], 1u);
+  __syncthreads();
+  if (t < 512) {
+    const uint32_t c = hist[t];
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[w] = incl;
+    tstart[t] = incl - c;
+  }
+  __syncthreads();
+  if (t < 512) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    tstart[t] += add;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IT; ++k)
+    if ((uint32_t)k * NT + t < tile_n) stage[tstart[dg[k]] + li[k]] = it[k];
+  __syncthreads();
+  for (uint32_t d = w; d < 512; d += NT / 64) {
+    const uint32_t s0 = tstart[d], c = hist[d];
+    const uint64_t g = goff[d];
+    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];
+  }
+}
+
 // SHEEP_BIN_TM=0: the digit-major counts and one flat scan (the previous layout).
 static bool bin_tile_major() {
   static const char* e = getenv("SHEEP_BIN_TM");
@@ -886,6 +944,12 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
   if (bin_tile_major()) {
     if (n == 0) return;
     tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
+    static const char* ebs = getenv("SHEEP_BIN_SCATTER");  // 0: the stable 8192-item scatter
+    if (!ebs || atoi(ebs) != 0) {
+      hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,
+                         in, out, n, (const uint32_t*)counts, digits);
+      return;
+    }
     hipLaunchKernelGGL((k_rsort_scatter<9, true, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in,
                        out, n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
     return;
