@@ -1164,7 +1164,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
                   uint32_t n_rank, uint32_t* __restrict__ pst, uint64_t* __restrict__ items,
                   uint32_t* err, int shift, uint32_t* __restrict__ counts, uint32_t ntiles,
                   const uint32_t* __restrict__ bins = nullptr, uint32_t nb = 0,
-                  uint16_t* __restrict__ digits = nullptr) {
+                  uint16_t* __restrict__ digits = nullptr, int plain = 0) {
   constexpr uint32_t NBIN = 1u << DB;
   __shared__ uint32_t hist[NBIN];
   __shared__ uint32_t sb[BINS ? NBIN : 1];
@@ -1214,8 +1214,12 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
     if (valid) items[idx] = ((uint64_t)hi << 32) | lo;
     uint32_t d = BINS ? bin_of(sb, nb, hi) : (hi >> shift) & (NBIN - 1);
     if (BINS && valid) digits[idx] = (uint16_t)d;  // the scatter pass reads it back
-    uint64_t match = digit_match<DB>(d, valid);
-    if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
+    if (plain) {  // hi bins are cut to similar record counts: few same-bin lanes per wave
+      if (valid) atomicAdd(&hist[d], 1u);
+    } else {
+      uint64_t match = digit_match<DB>(d, valid);
+      if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
+    }
   }
   __syncthreads();
   for (uint32_t i = t; i < NBIN; i += RS_THREADS)
@@ -1234,8 +1238,10 @@ void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank,
   if (!tm && nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
   auto k = tm ? (pre ? k_edge_pass_tiles<9, true, true, true> : k_edge_pass_tiles<9, false, true, true>)
               : (pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>);
+  static const char* epl = getenv("SHEEP_EP_PLAIN");  // bin counts by plain LDS atomics
+  const int plain = epl ? atoi(epl) : 1;
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
-                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits);
+                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits, plain);
 }
 
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
@@ -1250,7 +1256,7 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
                          : (tm ? k_edge_pass_tiles<8, false, false, true> : k_edge_pass_tiles<8, false>));
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
                      pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
-                     (uint16_t*)nullptr);
+                     (uint16_t*)nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------------------
