@@ -242,6 +242,14 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   uint64_t* items = (uint64_t*)c.scratch.get("seq_items", (size_t)n_ids * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_ids * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
+  static const char* ecz = getenv("SHEEP_SEQ_COMPACT");  // 0: sort all n_ids (zeros first)
+  if (!ecz || atoi(ecz) != 0) {
+    uint32_t* ptmp = (uint32_t*)c.scratch.get("seq_pack_tmp", pack_nz_tmp_words(n_ids) * 4);
+    launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
+    uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);
+    launch_unpack_seq(sorted, 0, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
+    return n_seq;
+  }
   launch_pack_deg(d_deg, n_ids, items, s);
   uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
   launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, selfc, mode);

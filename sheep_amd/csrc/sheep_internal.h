@@ -69,6 +69,10 @@ int rsort_first_width(int bits);
 uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t n, int bit_lo,
                          int bit_hi, uint32_t* tmp, hipStream_t s, bool counted0 = false);
 void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s);
+// (deg << 32 | id) of the ids with deg > 0 only, in id order; tmp: pack_nz_tmp_words(n) u32.
+size_t pack_nz_tmp_words(uint32_t n);
+void launch_pack_nonzero(const uint32_t* deg, uint32_t n, uint64_t* items, uint32_t* tmp,
+                         hipStream_t s);
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
                        uint32_t* rank, hipStream_t s, uint32_t* nsd = nullptr,
                        const uint32_t* selfc = nullptr, int file_mode = 0);

@@ -1044,6 +1044,65 @@ __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros,
   }
 }
 
+// The sequence holds only the ids with deg > 0 (sequence.h:55-61): pack just those, in id
+// order (a stable compaction: per-block counts, a scan, a block-local scan), so the radix
+// passes sort n_seq items instead of n_ids (half of them at RMAT-26).
+static constexpr uint32_t NZ_BLOCK = 4096;  // ids per block: 1024 threads x 4
+
+__global__ void __launch_bounds__(1024)
+k_nz_count(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, base = blockIdx.x * NZ_BLOCK + 4 * t;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c += (base + k < n && deg[base + k] != 0);
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((t & 63) == 0) wsum[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t sum = 0;
+    for (int i = 0; i < 16; ++i) sum += wsum[i];
+    bcnt[blockIdx.x] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+k_pack_nz(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __restrict__ bofs,
+          uint64_t* __restrict__ items) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, base = blockIdx.x * NZ_BLOCK + 4 * t;
+  uint32_t d[4], c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    d[k] = base + k < n ? deg[base + k] : 0u;
+    c += d[k] != 0;
+  }
+  const uint32_t incl = wave_incl_scan(c);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t pos = bofs[blockIdx.x] + incl - c;
+  for (uint32_t i = 0; i < w; ++i) pos += wsum[i];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (d[k]) items[pos++] = ((uint64_t)d[k] << 32) | (base + k);
+}
+
+size_t pack_nz_tmp_words(uint32_t n) {
+  const uint64_t nb = ((uint64_t)n + NZ_BLOCK - 1) / NZ_BLOCK;
+  return 2 * nb + scan_tmp_words(nb) + 2;
+}
+
+void launch_pack_nonzero(const uint32_t* deg, uint32_t n, uint64_t* items, uint32_t* tmp,
+                         hipStream_t s) {
+  if (n == 0) return;
+  const uint32_t nb = (uint32_t)(((uint64_t)n + NZ_BLOCK - 1) / NZ_BLOCK);
+  uint32_t* bcnt = tmp;
+  uint32_t* bofs = tmp + nb;
+  hipLaunchKernelGGL(k_nz_count, dim3(nb), dim3(1024), 0, s, deg, n, bcnt);
+  launch_scan_exclusive(bcnt, bofs, nb, bofs + nb, s);
+  hipLaunchKernelGGL(k_pack_nz, dim3(nb), dim3(1024), 0, s, deg, n, (const uint32_t*)bofs, items);
+}
+
 void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_pack_deg, dim3(grid_for(n)), dim3(BLOCK), 0, s, deg, n, items);
 }
