@@ -464,7 +464,7 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
               const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, uint32_t n_ids,
               uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
-              uint32_t* __restrict__ stats) {
+              uint32_t* __restrict__ stats, int plain) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -497,6 +497,10 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
           uint64_t ik = i + k;
           uint32_t v = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
           bool done = !(ik >= g0 && ik < g1);
+          if (plain) {  // no matching: repeated ids of a wave serialise in the LDS atomic unit
+            if (!done) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
+            continue;
+          }
           // one round of leader matching folds a hub's repeated id into one LDS add
           uint64_t act = __ballot(!done);
           if (act) {
@@ -561,6 +565,15 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 }
 
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
+// k_degb_hist16 without the per-wave leader matching of repeated ids (SHEEP_DEGB_PLAIN=0
+// restores it): ids are spread over 65536 counters per bucket, so a wave rarely repeats one,
+// and the match cost more than the serialised hub adds it saves (RMAT-26 hist 11.7 -> 10.7 ms
+// of degree phase, twitter-shape 15.6 -> 14.1 ms).
+static int degb_plain() {
+  static const char* e = getenv("SHEEP_DEGB_PLAIN");
+  return e ? atoi(e) : 1;
+}
+
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                             hipStream_t s, uint32_t* yhist, hipEvent_t counted, uint32_t* stats) {
@@ -614,7 +627,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   if (H > 1 && !(eh && atoi(eh) == 0))
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
-                       (const unsigned long long*)bstart, stats);
+                       (const unsigned long long*)bstart, stats, degb_plain());
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
