@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
             uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
-            uint32_t* __restrict__ stats) {
+            uint32_t* __restrict__ stats, int plain) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
@@ -429,6 +429,10 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
         uint32_t e = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
         bool done = !(ik >= s0 && ik < s1) || (H > 1 && (e >> 15) != h);
         uint32_t v = H > 1 ? (e & (DEGB_HALF - 1)) : e;
+        if (plain) {  // as k_degb_hist16
+          if (!done) atomicAdd(&cnt[v], 1u);
+          continue;
+        }
         // one round of leader matching folds a hub's repeated id into one LDS add
         uint64_t act = __ballot(!done);
         if (act) {
@@ -569,6 +573,9 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 // restores it): ids are spread over 65536 counters per bucket, so a wave rarely repeats one,
 // and the match cost more than the serialised hub adds it saves (RMAT-26 hist 11.7 -> 10.7 ms
 // of degree phase, twitter-shape 15.6 -> 14.1 ms).
+// bit 0: k_degb_hist16, bit 1: k_degb_hist.  The small-bucket histogram keeps the matching:
+// RMAT-22's 4096-id buckets repeat hub ids within a wave (degree 0.88 -> 0.94 ms plain), the
+// LJ shape gains (0.81 -> 0.72 ms).
 static int degb_plain() {
   static const char* e = getenv("SHEEP_DEGB_PLAIN");
   return e ? atoi(e) : 1;
@@ -627,11 +634,11 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   if (H > 1 && !(eh && atoi(eh) == 0))
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
-                       (const unsigned long long*)bstart, stats, degb_plain());
+                       (const unsigned long long*)bstart, stats, degb_plain() & 1);
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
-                       deg, (const unsigned long long*)bstart, stats);
+                       deg, (const unsigned long long*)bstart, stats, degb_plain() >> 1);
   return yhist != nullptr;
 }
 
