@@ -248,11 +248,13 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
     launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
     uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);
     launch_unpack_seq(sorted, 0, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
+    if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
     return n_seq;
   }
   launch_pack_deg(d_deg, n_ids, items, s);
   uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
   launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
+  if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
   return n_seq;
 }
 

@@ -76,6 +76,9 @@ void launch_pack_nonzero(const uint32_t* deg, uint32_t n, uint64_t* items, uint3
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
                        uint32_t* rank, hipStream_t s, uint32_t* nsd = nullptr,
                        const uint32_t* selfc = nullptr, int file_mode = 0);
+// nsd[rank[v]] -= w * selfc[v] (w = 2 in FILE mode): the self-loop part of launch_unpack_seq's nsd.
+void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t* rank,
+                          int file_mode, uint32_t* nsd, hipStream_t s);
 void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s);
 void launch_rank_scatter(const uint32_t* seq, uint32_t n_seq, uint32_t* rank, uint32_t* err,
                          hipStream_t s);

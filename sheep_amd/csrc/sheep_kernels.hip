@@ -1049,8 +1049,9 @@ __global__ void k_pack_deg(const uint32_t* __restrict__ deg, uint32_t n, uint64_
     items[i] = ((uint64_t)deg[i] << 32) | i;
 }
 
-// nsd (nullable): nsd[i] = degree - w * self-loop records of seq[i] (the non-self-loop
-// degree that pst needs), in rank order; the degree is the sorted item's key.
+// nsd (nullable): nsd[i] = degree of seq[i] in rank order (the sorted item's key); the
+// self-loop records are taken off afterwards by k_nsd_selfloops (rare: a sparse pass instead
+// of a gather per rank).
 __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros, uint32_t n_seq,
                              uint32_t* __restrict__ seq, uint32_t* __restrict__ rank,
                              uint32_t* __restrict__ nsd, const uint32_t* __restrict__ selfc,
@@ -1060,7 +1061,18 @@ __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros,
     uint32_t v = (uint32_t)it;
     seq[i] = v;
     if (rank) rank[v] = i;
-    if (nsd) nsd[i] = (uint32_t)(it >> 32) - w * selfc[v];
+    if (nsd) nsd[i] = (uint32_t)(it >> 32);
+  }
+}
+
+// nsd[rank[v]] -= w * selfc[v] for the ids with self-loop records (they have deg > 0, so a
+// rank): a coalesced read of selfc, random accesses only where it is non-zero.
+__global__ void k_nsd_selfloops(const uint32_t* __restrict__ selfc, uint32_t n_ids,
+                                const uint32_t* __restrict__ rank, uint32_t w,
+                                uint32_t* __restrict__ nsd) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_ids; v += gridDim.x * blockDim.x) {
+    const uint32_t c = selfc[v];
+    if (c) nsd[rank[v]] -= w * c;
   }
 }
 
@@ -1133,6 +1145,13 @@ void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, ui
   if (n_seq)
     hipLaunchKernelGGL(k_unpack_seq, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, items, zeros, n_seq,
                        seq, rank, nsd, selfc, file_mode ? 2u : 1u);
+}
+
+void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t* rank,
+                          int file_mode, uint32_t* nsd, hipStream_t s) {
+  if (n_ids)
+    hipLaunchKernelGGL(k_nsd_selfloops, dim3(grid_for(n_ids)), dim3(BLOCK), 0, s, selfc, n_ids, rank,
+                       file_mode ? 2u : 1u, nsd);
 }
 
 // ---------------------------------------------------------------------------------------
