@@ -2246,7 +2246,9 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   if (mapmode > 1) anchor = INV;
   if (e_end <= e_begin) return;
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
-  unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);
+  static const char* emg = getenv("SHEEP_KB_MGRID");  // blocks (2 per CU fit the LDS window)
+  static const uint64_t mgrid = emg ? (uint64_t)atoi(emg) : 512;
+  unsigned grid = (unsigned)std::min<uint64_t>(chunks, mgrid);
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
   static const char* ef = getenv("SHEEP_KB_MAPFIND");
   const int ro = ef && ef[0] == 'r';
