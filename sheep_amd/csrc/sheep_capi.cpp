@@ -82,6 +82,7 @@ static Ctx& init_ctx(int device) {
     HIP_CHECK(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     for (auto& e : c.kb_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : c.part_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&c.bins_ev, hipEventDisableTiming));
     HIP_CHECK(hipMalloc(&c.d_err, 16));
     HIP_CHECK(hipMemset(c.d_err, 0, 16));
     HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
@@ -523,6 +524,27 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
   bool part = use_part(m);
   const uint32_t* src = d_uv;
+  // Hi bins (one scatter pass) when the degrees are at hand; else the two-pass radix sort.
+  const char* esort = getenv("SHEEP_SORT");
+  const bool use_bins = kb && pst_count && m >= (1ull << 20) && n_seq > 256 &&
+                        !(esort && strcmp(esort, "radix") == 0);
+  // The bins come from the chunk degree sums (seq order): they are summed and copied to the
+  // host BEFORE the second partition pass is enqueued, so the host cuts the bins while the GPU
+  // runs that pass instead of idling for the round trip.
+  const size_t nch = ((size_t)n_seq + 255) / 256;
+  if (use_bins) {
+    uint64_t* cds = (uint64_t*)c.scratch.get("chunk_deg", nch * 8);
+    launch_chunk_degsum(di->seq, di->deg, n_seq, cds, s, di->nsd);
+    if (c.h_chunks_n < nch) {
+      if (c.h_chunks) HIP_CHECK(hipHostFree(c.h_chunks));
+      c.h_chunks = nullptr;
+      c.h_chunks_n = 0;
+      HIP_CHECK(hipHostMalloc((void**)&c.h_chunks, nch * 8, hipHostMallocDefault));
+      c.h_chunks_n = nch;
+    }
+    HIP_CHECK(hipMemcpyAsync(c.h_chunks, cds, nch * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(c.bins_ev, s));
+  }
   if (part) {
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
@@ -534,22 +556,14 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
   }
-  // Hi bins (one scatter pass) when the degrees are at hand; else the two-pass radix sort.
-  const char* esort = getenv("SHEEP_SORT");
-  const bool use_bins = kb && pst_count && m >= (1ull << 20) && n_seq > 256 &&
-                        !(esort && strcmp(esort, "radix") == 0);
   const uint64_t* sorted;
   uint64_t* spare;
   Buckets given;
   const uint32_t* dbins = nullptr;
   uint32_t nbins = 0;
   if (use_bins) {
-    const size_t nch = ((size_t)n_seq + 255) / 256;
-    uint64_t* cds = (uint64_t*)c.scratch.get("chunk_deg", nch * 8);
-    launch_chunk_degsum(di->seq, di->deg, n_seq, cds, s, di->nsd);
-    std::vector<uint64_t> hd(nch);
-    HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipEventSynchronize(c.bins_ev));
+    std::vector<uint64_t> hd(c.h_chunks, c.h_chunks + nch);
     std::vector<uint32_t> bounds = make_bins(hd, n_seq);
     nbins = (uint32_t)bounds.size();
     uint32_t* db = (uint32_t*)c.scratch.get("hi_bins", 512 * 4);

@@ -32,6 +32,9 @@ struct Ctx {
   hipStream_t side = nullptr;     // second stream of the pipelined kb loop
   hipEvent_t kb_ev[5] = {};       // kb loop: [0,1] map done, [2,3] apply done (by parity), [4] start
   hipEvent_t part_ev[2] = {};     // graph2tree: [0] degree done, [1] first partition pass done
+  hipEvent_t bins_ev = nullptr;   // the chunk degree sums reached the pinned host buffer
+  uint64_t* h_chunks = nullptr;   // pinned host buffer for them (grown on demand)
+  size_t h_chunks_n = 0;
   Scratch scratch;
   uint32_t* d_err = nullptr;     // device error word
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
