@@ -83,6 +83,7 @@ static Ctx& init_ctx(int device) {
     for (auto& e : c.kb_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : c.part_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&c.bins_ev, hipEventDisableTiming));
+    HIP_CHECK(hipHostMalloc((void**)&c.h_bstart, 513 * 8, hipHostMallocDefault));
     HIP_CHECK(hipMalloc(&c.d_err, 16));
     HIP_CHECK(hipMemset(c.d_err, 0, 16));
     HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
@@ -573,10 +574,10 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_edge_pass_bins(src, m, d_rank, n_rank, items, c.d_err, db, nbins, tmp, digits, s, part);
     if (tm) tm->mark("edge_pass");
     unsigned long long* dstart = (unsigned long long*)c.scratch.get("bin_start", 513 * 8);
-    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, digits, s);
-    std::vector<unsigned long long> hs(nbins + 1);
-    HIP_CHECK(hipMemcpyAsync(hs.data(), dstart, (nbins + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    // the bin starts reach the host before the scatter runs: the buckets are cut meanwhile
+    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, digits, s, c.h_bstart, c.bins_ev);
+    HIP_CHECK(hipEventSynchronize(c.bins_ev));
+    std::vector<unsigned long long> hs(c.h_bstart, c.h_bstart + nbins + 1);
     given = buckets_from_bins(bounds, hs, m, n_seq);
     sorted = items_b;
     spare = items;

@@ -34,6 +34,7 @@ struct Ctx {
   hipEvent_t part_ev[2] = {};     // graph2tree: [0] degree done, [1] first partition pass done
   hipEvent_t bins_ev = nullptr;   // the chunk degree sums reached the pinned host buffer
   uint64_t* h_chunks = nullptr;   // pinned host buffer for them (grown on demand)
+  unsigned long long* h_bstart = nullptr;  // pinned: the 513 bin starts of the scatter
   size_t h_chunks_n = 0;
   Scratch scratch;
   uint32_t* d_err = nullptr;     // device error word
@@ -103,7 +104,9 @@ void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank,
                            uint32_t* tmp, uint16_t* digits, hipStream_t s, bool pre);
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
                   uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
-                  hipStream_t s);
+                  hipStream_t s,
+                  unsigned long long* h_start = nullptr /* pinned: bin_start, before the scatter */,
+                  hipEvent_t started = nullptr /* recorded once h_start is written */);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,

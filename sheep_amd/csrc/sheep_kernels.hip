@@ -958,12 +958,20 @@ static bool bin_tile_major() {
 
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
                   uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
-                  hipStream_t s) {
+                  hipStream_t s, unsigned long long* h_start, hipEvent_t started) {
+  // the bin starts are known before the scatter: the caller may read them while it runs
+  auto publish = [&]() {
+    if (h_start) {
+      (void)hipMemcpyAsync(h_start, bin_start, (size_t)(nb + 1) * 8, hipMemcpyDeviceToHost, s);
+      (void)hipEventRecord(started, s);
+    }
+  };
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   if (bin_tile_major()) {
     if (n == 0) return;
     tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
+    publish();
     static const char* ebs = getenv("SHEEP_BIN_SCATTER");  // 0: the stable 8192-item scatter
     if (!ebs || atoi(ebs) != 0) {
       hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,
@@ -978,6 +986,7 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
   launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
   hipLaunchKernelGGL(k_bin_starts, dim3(3), dim3(BLOCK), 0, s, (const uint32_t*)counts, (uint32_t)nt,
                      nb, n, bin_start);
+  publish();
   if (n)
     hipLaunchKernelGGL((k_rsort_scatter<9, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in, out,
                        n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
