@@ -80,6 +80,34 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("scale,seed,mode,env", [
+    (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
+    (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
+    (16, 23, 0, {"SHEEP_EDGE_PART": "1"}),  # the partitioned gathers at a small size
+    (16, 24, 0, {"SHEEP_EDGE_PART": "0"}),  # direct gathers, hi bins
+])
+def test_graph2tree_dev_front_half(oracle, gpu, monkeypatch, scale, seed, mode, env):
+    """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
+    and the first partition pass runs beside the degree pass and the sequence sort, with the
+    compacted sequence sort, tile-major bin counts and the unstable bin scatter: seq, parent
+    and pst bit-exact against the checker in both degree conventions."""
+    import torch
+    from sheep_amd import device
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    uv_d = device.rmat(scale, 16, seed)
+    uv = uv_d.cpu().numpy().view(np.uint32)
+    seq = oracle.degree_sequence(uv, mode)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << scale, mode)
+    torch.cuda.synchronize()
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("n,m,gamma,i0,seed", [(1000, 20000, 2.3, 100.0, 3),
                                                (65536, 1 << 20, 2.1, 50.0, 5),
                                                (300001, 1 << 21, 2.3, 100.0, 7)])
