@@ -17,6 +17,10 @@
  *
  * Types follow lib/defs.h:76-82: ids, jnids and weights are uint32, INVALID = 0xFFFFFFFF.
  * An edge stream is m records of (tail, head) as 2*m uint32 (the XS1 weight is dropped).
+ *
+ * Size limits (offsets and counters are u32): a tree build takes m < 2^32 records, a degree
+ * pass (2m endpoints) m < 2^31, the partition evaluation 2m < 2^32 adjacency entries; larger
+ * inputs return -EINVAL.  Shard them (-l n/k + merge, or the multi-GPU entry points).
  */
 #ifndef SHEEP_AMD_H
 #define SHEEP_AMD_H
@@ -198,6 +202,18 @@ int sheep_rmat_dev(uint32_t* d_uv, int scale, uint64_t seed, uint64_t e_begin, u
  * Enqueue only. */
 int sheep_powerlaw_dev(uint32_t* d_uv, uint32_t n, double gamma, double i0, uint64_t seed,
                        uint64_t e_begin, uint64_t e_end, void* stream);
+
+/* ---- host-side partition (the reference keeps it on the host) ---------------------------- */
+
+/* Partition(seq, jnodes, k, balance, false, true, false) (partition.cpp:50-67 ->
+ * forwardPartition :86-157, pst weights) for each k of ks[0..n_k) in turn on ONE table, as
+ * partition_tree does (partition_tree.cpp:130-146): the kids lists that one k sorts in place
+ * are the starting order of the next.  parent/pst: the n_seq jnodes; seq: the n_seq ids;
+ * parts_out: n_k * n_vid int16, vid-indexed (-1 = INVALID_PART for ids not in seq), n_vid >=
+ * max(seq) + 1; created_out (nullable): n_k part counts ("Actually created").  Host only. */
+int sheep_partition(const uint32_t* parent, const uint32_t* pst, uint32_t n_seq,
+                    const uint32_t* seq, const int32_t* ks, uint32_t n_k, double balance,
+                    int16_t* parts_out, uint32_t n_vid, uint32_t* created_out);
 
 /* Kernel timing of the last synchronising call (ms per named phase), for bench/profiling.
  * Fills up to cap (name, ms) pairs; returns the count. */

@@ -177,3 +177,19 @@ def graph2tree(uv, mode=DEGREE_LLAMA):
     """graph2tree's serial path (graph2tree.cpp:162-193): degreeSequence + JTree."""
     seq = degree_sequence(uv, mode)
     return seq, build_tree(uv, seq)
+
+
+# ---- partition (host, as in the reference) ---------------------------------------------------
+
+def partition(tree, seq, ks, balance=1.03):
+    """Partition(seq, jnodes, k, balance) (partition.cpp:50-67 -> forwardPartition :86-157) for
+    each k of ``ks`` in turn on ONE table, as partition_tree runs its k list.  Returns a list of
+    vid-indexed int16 part arrays (-1 for ids not in seq) and the created part counts."""
+    seq = np.ascontiguousarray(seq, np.uint32)
+    ks = np.ascontiguousarray(np.atleast_1d(ks), np.int32)
+    n_vid = int(seq.max()) + 1 if seq.size else 0
+    parts = np.empty((ks.size, max(n_vid, 1)), np.int16)
+    created = np.zeros(ks.size, np.uint32)
+    capi.call("sheep_partition", _ptr(tree.parent), _ptr(tree.pst), tree.size(), _ptr(seq),
+              _ptr(ks), ks.size, float(balance), _ptr(parts), n_vid, _ptr(created))
+    return [parts[i, :n_vid] for i in range(ks.size)], [int(c) for c in created]

@@ -83,6 +83,8 @@ def lib():
         "sheep_ls_apply": [vp, c.c_uint32, vp, c.c_uint32, c.c_uint32, vp],
         "sheep_ls_finish": [vp, u32p, u32p, u32p, c.c_int, u32p, u32p, vp],
         "sheep_ls_free": [vp],
+        "sheep_partition": [u32p, u32p, c.c_uint32, u32p, vp, c.c_uint32, c.c_double, vp,
+                            c.c_uint32, vp],
     }
     for name, args in sigs.items():
         f = getattr(L, name)

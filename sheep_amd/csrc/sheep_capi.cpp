@@ -21,6 +21,7 @@
 namespace sheep {
 
 static thread_local std::string g_last_error;
+void set_last_error(const char* msg) { g_last_error = msg; }
 static thread_local int g_device = -1;
 static Ctx g_ctx[64];
 static std::mutex g_mu;
@@ -179,6 +180,17 @@ static void check_err(Ctx& c, hipStream_t s) {
   }
 }
 
+// Counters, tile offsets and kept-pair positions of the tree build are u32 (records), and the
+// degree pass's endpoint offsets are u32 (2 per record): reject inputs beyond them.
+static void require_records(uint64_t m, const char* what) {
+  if (m >= (1ull << 32))
+    throw ApiError(-EINVAL, std::string(what) + ": at most 2^32 - 1 records (u32 offsets)");
+}
+static void require_endpoints(uint64_t m, const char* what) {
+  if (2 * m >= (1ull << 32))
+    throw ApiError(-EINVAL, std::string(what) + ": at most 2^31 - 1 records (u32 endpoint offsets)");
+}
+
 static inline int bits_for(uint64_t v) {  // number of significant bits
   int b = 0;
   while (v) { ++b; v >>= 1; }
@@ -200,6 +212,7 @@ static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
     if (stats) launch_deg_stats(d_deg, n_ids, stats, s);
     return false;
   }
+  require_endpoints(m, "degree");
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
   uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
   return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist,
@@ -413,8 +426,10 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
     D += (double)dsum[c];
     W += w[c];
   }
-  double wmax = W / 320, wide = W / 50000;
   std::vector<uint32_t> b;
+  // No estimated records (every record a self-loop, or no degrees): one bin holds them all.
+  if (!(tot > 0) || !(W > 0) || nch < 2) return {0u, n_seq};
+  double wmax = W / 320, wide = W / 50000;
   for (int attempt = 0; attempt < 32; ++attempt) {
     b.assign(1, 0u);
     double acc = 0;
@@ -430,7 +445,16 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
     wide *= 2;
     wmax *= 1.25;
   }
+  // Hard cap (the bin digit, the LDS tables of the scatter and the bin-start buffers hold 512
+  // entries): keep every s-th bound.  Any bounds give the same tree; only the work shifts.
+  if (b.size() + 1 > 512) {
+    const size_t st = (b.size() + 510) / 511;
+    std::vector<uint32_t> c;
+    for (size_t i = 0; i < b.size(); i += st) c.push_back(b[i]);
+    b.swap(c);
+  }
   b.push_back(n_seq);
+  if (b.size() > 512) throw ApiError(-EIO, "make_bins: more than 512 hi bins");
   return b;
 }
 
@@ -499,6 +523,7 @@ static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
 static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                            uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
                            hipStream_t s, Timer* tm, const DegInfo* di = nullptr) {
+  require_records(m, "tree build");
   if (n_seq == 0) return;
   launch_fill(d_parent, INV, n_seq, s);
   launch_fill(d_pst, 0, n_seq, s);
@@ -619,6 +644,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
 // (v, parent_t[v]) as items, sorted by parent, through the kb loop.
 static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uint32_t n,
                               uint32_t* d_parent, hipStream_t s, Timer* tm) {
+  require_records((uint64_t)T * n, "forest merge");
   if (n == 0) return;
   launch_fill(d_parent, INV, n, s);
   uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n * 4);
@@ -703,6 +729,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
                      uint32_t* d_err, hipStream_t s) {
+  require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
   L.n_seq = n_seq;
@@ -930,6 +957,7 @@ int sheep_gpu_init(int device) {
 int sheep_release(void) {
   API_BEGIN
   Ctx& c = ctx();
+  if (c.ls_live > 0) throw ApiError(-EBUSY, "sheep_release: a lockstep session is live");
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.scratch.release();
   API_END

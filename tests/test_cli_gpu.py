@@ -92,8 +92,22 @@ def test_graph2tree_partition_output(gpu, oracle, hep_edges, tmp_path):
     seq = oracle.degree_sequence(hep_edges)
     p, s = oracle.build_tree(hep_edges, seq)
     parts = oracle.PartTree(p, s).partition(seq, 4)
-    n = sum(1 for q in range(4) for _ in open("%s%04d" % (prefix, q)))
-    assert n == len(hep_edges)
+    # writePartitionedGraph (partition.cpp:588-630): every record (X, Y), X < Y once (self-loops
+    # skipped), to the part of its lower-sequence endpoint; compared as per-file multisets
+    # (the line order follows LLAMA's adjacency order, which no reference fixture pins)
+    pos = np.full(parts.size, -1, np.int64)
+    pos[seq] = np.arange(seq.size)
+    x = hep_edges.min(axis=1).astype(np.int64)
+    y = hep_edges.max(axis=1).astype(np.int64)
+    keep = x != y
+    x, y = x[keep], y[keep]
+    owner = np.where(pos[x] < pos[y], parts[x], parts[y])
+    created = int(parts.max()) + 1
+    for q in range(created):
+        lines = sorted(tuple(int(v) for v in l.split()) for l in open("%s%04d" % (prefix, q)))
+        want = sorted(zip(x[owner == q].tolist(), y[owner == q].tolist()))
+        assert lines == want, q
+    assert not os.path.exists("%s%04d" % (prefix, created))
 
 
 def test_partition_tree_gpu_evaluation_prints_the_same(gpu, tmp_path):
