@@ -56,6 +56,15 @@ const char* sheep_last_error(void);
 /* ABI version: (major << 16) | minor. */
 int sheep_abi_version(void);
 
+/* Tuning options (sheep_amd/csrc/sheep_internal.h, struct Knobs): they move work between
+ * kernels and never change a result.  Their defaults come from SHEEP_<NAME> environment
+ * variables, read ONCE when the library first initialises a device; afterwards only these
+ * calls change them (process-wide).  Names: degree, edge_part, part_overlap, seq_compact,
+ * sort, kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, degb_plain, degb_hist, bin_tm,
+ * bin_scatter, ep_plain, tree_stats.  -EINVAL for an unknown name. */
+int sheep_set_option(const char* name, long long value);
+int sheep_get_option(const char* name, long long* value);
+
 /* ---- host-pointer API (synchronous; what the reference's lib/ would bind) --------------- */
 
 /* Degree sequence: the ids with degree>0 ordered by (degree asc, id asc).

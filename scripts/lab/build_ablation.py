@@ -1,0 +1,89 @@
+"""Build a lab copy of libsheep_amd.so with one k_kb_map ablation (results WRONG, timing only):
+    python scripts/lab/build_ablation.py NAME  -> scripts/lab/libsheep_NAME.so
+Ablations patch the kernel text of a temporary copy; the product source is not touched."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SRC = os.path.join(ROOT, "sheep_amd", "csrc")
+
+PATCHES = {
+    "base": [],
+    "nt": [("      nx[r] = idx < c1 ? items[idx] : 0ull;", "      nx[r] = idx < c1 ? __builtin_nontemporal_load(&items[idx]) : 0ull;"),
+           ("      if (it[r] != ~0ull) kept[pos + __popcll(bal & lt)] = it[r];", "      if (it[r] != ~0ull) __builtin_nontemporal_store(it[r], &kept[pos + __popcll(bal & lt)]);")],
+    "r16": [("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 16384;")],
+    "r12": [("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 12288;")],
+    "r16np": [("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 16384;"),
+              ("    if (more) fetch(c0 + KM_CHUNK);  // issued after the bitmap loads", "")],
+    # s_memtime stamps of thread 0 per map phase, summed into the stats words (run with
+    # SHEEP_TREE_STATS=1; the capi's tree_stats line then prints them)
+    "stamp": [("  uint32_t since_flush = 0;\n", "  uint32_t since_flush = 0;\n  unsigned long long T0 = 0, T1 = 0, ph[7] = {0,0,0,0,0,0,0};\n"),
+              ("    uint64_t it[R];\n    uint32_t vmask = 0;\n#pragma unroll\n    for (int r = 0; r < R; ++r) {\n      it[r] = nx[r];",
+               "    T0 = __builtin_amdgcn_s_memtime();\n    uint64_t it[R];\n    uint32_t vmask = 0;\n#pragma unroll\n    for (int r = 0; r < R; ++r) {\n      it[r] = nx[r];"),
+              ("    if (STATS) misses += (uint64_t)__popc(miss);\n",
+               "    if (STATS) misses += (uint64_t)__popc(miss);\n    T1 = __builtin_amdgcn_s_memtime(); ph[0] += T1 - T0; T0 = T1;\n"),
+              ("    // 3. roots -> giant (and its bit)", "    T1 = __builtin_amdgcn_s_memtime(); ph[1] += T1 - T0; T0 = T1;\n    // 3. roots -> giant (and its bit)"),
+              ("    uint32_t nout = 0;\n", "    uint32_t nout = 0;\n    T1 = __builtin_amdgcn_s_memtime(); ph[2] += T1 - T0; T0 = T1;\n"),
+              ("    if (lane == 0) woff[w] = nout;\n", "    if (lane == 0) woff[w] = nout;\n    T1 = __builtin_amdgcn_s_memtime(); ph[3] += T1 - T0; T0 = T1;\n"),
+              ("    if (flush) {\n      since_flush = 0;", "    T1 = __builtin_amdgcn_s_memtime(); ph[4] += T1 - T0; T0 = T1;\n    if (flush) {\n      since_flush = 0;"),
+              ("    // compaction: one reservation per chunk", "    T1 = __builtin_amdgcn_s_memtime(); ph[5] += T1 - T0; T0 = T1;\n    // compaction: one reservation per chunk"),
+              ("    // no barrier here: the next chunk", "    T1 = __builtin_amdgcn_s_memtime(); ph[6] += T1 - T0; T0 = T1;\n    // no barrier here: the next chunk"),
+              ("    atomicAdd(&stats[7], (unsigned long long)misses);\n",
+               "    atomicAdd(&stats[7], (unsigned long long)misses);\n    if (t == 0) { atomicAdd(&stats[1], ph[0]); atomicAdd(&stats[2], ph[1]); atomicAdd(&stats[3], ph[2]); atomicAdd(&stats[4], ph[3]); atomicAdd(&stats[13], ph[4]); atomicAdd(&stats[14], ph[5]); atomicAdd(&stats[15], ph[6]); }\n")],
+    # smaller map blocks: more chunks in flight per CU (correct results)
+    "b256": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 256;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 2048; "),
+             ("static constexpr uint32_t KM_WIN = 32768;", "static constexpr uint32_t KM_WIN = 8192;"),
+             ("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 1280);")],
+    "b512": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 512;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 4096; "),
+             ("static constexpr uint32_t KM_WIN = 32768;", "static constexpr uint32_t KM_WIN = 16384;"),
+             ("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 768);")],
+    "b256w16": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 256;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 2048; "),
+             ("static constexpr uint32_t KM_WIN = 32768;", "static constexpr uint32_t KM_WIN = 16384;"),
+             ("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 1024);")],
+    # no hi counts at all (pst wrong)
+    "nocnt": [("if (valid && cnt) {", "if (false) {"),
+              ("    if (cnt)\n      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {\n        uint32_t v = wcnt[i];",
+               "    if (false)\n      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {\n        uint32_t v = wcnt[i];")],
+    # counts kept in LDS only (no global flush)
+    "noflush": [("        if (v & 0xFFFFu) atomicAdd(&cnt[bbase + 2 * i], v & 0xFFFFu);\n        if (v >> 16) atomicAdd(&cnt[bbase + 2 * i + 1], v >> 16);",
+                 "        if (v == 0xFFFFFFFFu) cnt[0] = v;")],
+    # no kept writes
+    "nokept": [("      if (it[r] != ~0ull) kept[pos + __popcll(bal & lt)] = it[r];", "      if (it[r] == 1ull) kept[0] = it[r];")],
+    # no finds: every miss is taken as giant
+    "nofind": [("    for (uint32_t act = miss; act;) {", "    for (uint32_t act = 0; act;) {")],
+}
+
+
+def main():
+    name = sys.argv[1]
+    text = open(os.path.join(SRC, "sheep_kernels.hip")).read()
+    for a, b in PATCHES[name]:
+        assert a in text, a
+        text = text.replace(a, b)
+    capi = open(os.path.join(SRC, "sheep_capi.cpp")).read()
+    if name == "stamp":
+        a = 'h[0], h[5], h[7], h[8], h[9], h[10], h[11], h[12]);'
+        assert a in capi
+        capi = capi.replace(a, a + '\n    fprintf(stderr, "map_phases_cycles load+bits %llu finds %llu label %llu lds %llu barA %llu flush %llu compact+barB+write %llu\\n", h[1], h[2], h[3], h[4], h[13], h[14], h[15]);')
+    tmp = "/tmp/sheep_lab_%s" % name
+    os.makedirs(tmp, exist_ok=True)
+    for f in ("powerlaw.h", "rmat.h", "sheep_internal.h"):
+        open(os.path.join(tmp, f), "w").write(open(os.path.join(SRC, f)).read())
+    open(os.path.join(tmp, "sheep_kernels.hip"), "w").write(text)
+    open(os.path.join(tmp, "sheep_capi.cpp"), "w").write(capi.replace('"../../include/sheep_amd.h"', '"%s"' % os.path.join(ROOT, "include", "sheep_amd.h")))
+    out = os.path.join(ROOT, "scripts", "lab", "libsheep_%s.so" % name)
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
+           "-Wno-unused-result", "-shared", "-o", out, "-I", SRC, "-x", "hip",
+           os.path.join(tmp, "sheep_kernels.hip"), "-x", "hip", os.path.join(SRC, "sheep_eval.hip"),
+           "-x", "hip", os.path.join(tmp, "sheep_capi.cpp"), "-x", "hip",
+           os.path.join(SRC, "sheep_host.cpp")]
+    subprocess.run(cmd, check=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

@@ -83,6 +83,8 @@ def lib():
         "sheep_ls_apply": [vp, c.c_uint32, vp, c.c_uint32, c.c_uint32, vp],
         "sheep_ls_finish": [vp, u32p, u32p, u32p, c.c_int, u32p, u32p, vp],
         "sheep_ls_free": [vp],
+        "sheep_set_option": [c.c_char_p, c.c_longlong],
+        "sheep_get_option": [c.c_char_p, c.c_void_p],
         "sheep_partition": [u32p, u32p, c.c_uint32, u32p, vp, c.c_uint32, c.c_double, vp,
                             c.c_uint32, vp],
     }
@@ -109,3 +111,11 @@ def last_timings():
     ms = (ctypes.c_double * 32)()
     n = L.sheep_last_timings(names, ms, 32)
     return [(names[i].decode(), ms[i]) for i in range(n)]
+
+
+def set_option(name, value):
+    """sheep_set_option: a tuning option (results never depend on it); returns the old value."""
+    old = ctypes.c_longlong(0)
+    call("sheep_get_option", name.encode(), ctypes.byref(old))
+    call("sheep_set_option", name.encode(), int(value))
+    return old.value

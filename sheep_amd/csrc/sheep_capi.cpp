@@ -26,6 +26,45 @@ static thread_local int g_device = -1;
 static Ctx g_ctx[64];
 static std::mutex g_mu;
 
+// ---- options (sheep_internal.h Knobs): SHEEP_<NAME> once, then sheep_set_option ----------
+struct KnobDef {
+  const char* name;
+  int Knobs::*field;
+};
+static const KnobDef kKnobs[] = {
+    {"degree", &Knobs::degree},           {"edge_part", &Knobs::edge_part},
+    {"part_overlap", &Knobs::part_overlap}, {"seq_compact", &Knobs::seq_compact},
+    {"sort", &Knobs::sort_radix},         {"kb_buckets", &Knobs::kb_buckets},
+    {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
+    {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},
+    {"degb_plain", &Knobs::degb_plain},   {"degb_hist", &Knobs::degb_hist16},
+    {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
+    {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
+};
+
+static Knobs g_knobs;
+static std::once_flag g_knobs_once;
+
+static void load_knobs_from_env() {
+  for (const KnobDef& d : kKnobs) {
+    std::string env = "SHEEP_";
+    for (const char* q = d.name; *q; ++q) env += (char)toupper(*q);
+    const char* v = getenv(env.c_str());
+    if (!v) continue;
+    if (d.field == &Knobs::degree)  // "atomic" / "bucketed" (or the number)
+      g_knobs.degree = !strcmp(v, "atomic") ? 1 : !strcmp(v, "bucketed") ? 2 : atoi(v);
+    else if (d.field == &Knobs::sort_radix)
+      g_knobs.sort_radix = !strcmp(v, "radix") ? 1 : atoi(v);
+    else
+      g_knobs.*d.field = atoi(v);
+  }
+}
+
+Knobs& knobs() {
+  std::call_once(g_knobs_once, load_knobs_from_env);
+  return g_knobs;
+}
+
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
@@ -77,6 +116,7 @@ static Ctx& init_ctx(int device) {
   if (device < 0 || device >= 64) throw ApiError(-EINVAL, "device index out of range");
   std::lock_guard<std::mutex> lk(g_mu);
   Ctx& c = g_ctx[device];
+  (void)knobs();  // the environment is read once, here
   HIP_CHECK(hipSetDevice(device));
   if (c.device < 0) {
     HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
@@ -205,8 +245,8 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int mode,
                        uint32_t* d_deg, uint32_t* d_selfc, hipStream_t s, bool want_yhist = false,
                        hipEvent_t counted = nullptr, uint32_t* stats = nullptr) {
-  const char* e = getenv("SHEEP_DEGREE");
-  bool bucketed = e ? strcmp(e, "bucketed") == 0 : (m >= (1ull << 18));
+  const int kd = knobs().degree;
+  bool bucketed = kd == 0 ? m >= (1ull << 18) : kd == 2;
   if (!bucketed || n_ids == 0) {
     launch_degree(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, s);
     if (stats) launch_deg_stats(d_deg, n_ids, stats, s);
@@ -233,8 +273,8 @@ struct DegInfo {
 
 // Rank gathers in partitioned order (launch_part_gather) for large inputs.
 static bool use_part(uint64_t m) {
-  const char* ep = getenv("SHEEP_EDGE_PART");
-  return ep ? atoi(ep) != 0 : m >= (1ull << 22);
+  const int ep = knobs().edge_part;
+  return ep < 0 ? m >= (1ull << 22) : ep != 0;
 }
 
 // stats_ready: the degree pass already wrote max degree / zero-degree count to "stats".
@@ -257,8 +297,7 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   uint64_t* items = (uint64_t*)c.scratch.get("seq_items", (size_t)n_ids * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_ids * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
-  static const char* ecz = getenv("SHEEP_SEQ_COMPACT");  // 0: sort all n_ids (zeros first)
-  if (!ecz || atoi(ecz) != 0) {
+  if (knobs().seq_compact) {  // 0: sort all n_ids (zeros first)
     uint32_t* ptmp = (uint32_t*)c.scratch.get("seq_pack_tmp", pack_nz_tmp_words(n_ids) * 4);
     launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
     uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);
@@ -274,7 +313,7 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
 }
 
 // Liu's elimination tree from items sorted by hi down to groups of 2^lo_bit ranks (m items,
-// INVALID his last): the kb bucket loop (or the plain zipper).  parent: n_seq words, INVALID
+// INVALID his last): the kb bucket loop.  parent: n_seq words, INVALID
 // filled; jump: n_seq zeroed words; spare: m free u64 (kept pairs); hcnt: nullable hi counts.
 // Bucket boundaries (rank, first record) of a kb loop, ending with (n_seq, m_valid).
 using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
@@ -287,125 +326,133 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 // critical path is the apply (RMAT-26, P = 8 simulation: K = 40/48/56/64 -> apply
 // 18.8/18.7/19.2/20.5 ms).
 static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 48) {
-  const char* ek = getenv("SHEEP_KB_BUCKETS");
-  const char* er = getenv("SHEEP_KB_RANKB");
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
-  *K_e = ek ? (uint32_t)atoi(ek) : K_auto;
-  *K_r = er ? (uint32_t)atoi(er) : K_auto;
+  *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : K_auto;
+  *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
 }
 
 static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, uint64_t m,
                              uint32_t n_seq, int lo_bit, uint32_t* d_parent, uint32_t* jump,
-                             uint32_t* hcnt, bool kb, bool stats, unsigned long long* ws,
-                             hipStream_t s, Timer* tm, const Buckets* given = nullptr,
+                             uint32_t* hcnt, bool stats, unsigned long long* ws, hipStream_t s,
+                             Timer* tm, const Buckets* given = nullptr,
                              const uint32_t* bins = nullptr, uint32_t nb = 0) {
-  const char* es = getenv("SHEEP_TREE_STATS");
-  if (!kb) {
-    const char* ev = getenv("SHEEP_TREE_VARIANT");
-    int variant = ev ? atoi(ev) : 4 + 8;  // agent loads, jump hints, lane work queue
-    launch_tree_insert(sorted, m, d_parent, jump, variant, stats, ws, s);
+  uint32_t K_e, K_r;
+  kb_counts(m, &K_e, &K_r);
+  uint32_t K = K_e + K_r;
+  uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
+  uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
+  uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
+  uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 2 * 64);
+  const size_t bm_words = (size_t)n_seq / 32 + 2, spq_words = (size_t)n_seq / 32 + 64;
+  uint32_t* bitmaps = (uint32_t*)c.scratch.get("kb_bitmap", 2 * bm_words * 4);
+  uint32_t* spqs = (uint32_t*)c.scratch.get("kb_spq", 2 * spq_words * 4);
+  // giant bitmap (k_kb_map) and the two slots of its reference vertex (INV: none yet)
+  uint32_t* gbits = (uint32_t*)c.scratch.get("kb_gbits", bm_words * 4);
+  uint32_t* gx = (uint32_t*)c.scratch.get("kb_gx", 2 * 4);
+  (void)hipMemsetAsync(counters, 0, 2 * 64, s);
+  (void)hipMemsetAsync(bitmaps, 0, 2 * bm_words * 4, s);
+  (void)hipMemsetAsync(gx, 0xFF, 2 * 4, s);
+  unsigned long long* bounds =
+      (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
+  launch_iota(uf, n_seq, s);
+  launch_iota(label, n_seq, s);
+  (void)hipMemsetAsync(ws, 0, 64 * 2, s);
+  Buckets bk;
+  uint64_t m_valid = 0;
+  if (given) {
+    bk = *given;
+    m_valid = bk.back().second;
   } else {
-    uint32_t K_e, K_r;
-    kb_counts(m, &K_e, &K_r);
-    uint32_t K = K_e + K_r;
-    uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
-    uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
-    uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
-    uint32_t* counters = (uint32_t*)c.scratch.get("kb_counters", 2 * 64);
-    const size_t bm_words = (size_t)n_seq / 32 + 2, spq_words = (size_t)n_seq / 32 + 64;
-    uint32_t* bitmaps = (uint32_t*)c.scratch.get("kb_bitmap", 2 * bm_words * 4);
-    uint32_t* spqs = (uint32_t*)c.scratch.get("kb_spq", 2 * spq_words * 4);
-    (void)hipMemsetAsync(counters, 0, 2 * 64, s);
-    (void)hipMemsetAsync(bitmaps, 0, 2 * bm_words * 4, s);
-    unsigned long long* bounds =
-        (unsigned long long*)c.scratch.get("kb_bounds", (size_t)(K + 1) * 16);
-    launch_iota(uf, n_seq, s);
-    launch_iota(label, n_seq, s);
-    (void)hipMemsetAsync(ws, 0, 64 * 2, s);
-    Buckets bk;
-    uint64_t m_valid = 0;
-    if (given) {
-      bk = *given;
-      m_valid = bk.back().second;
-    } else {
-      launch_kb_bounds(sorted, m, K_e, K_r, n_seq, lo_bit, bounds, s);
-      std::vector<unsigned long long> hb(2 * (K + 1));
-      HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
-      HIP_CHECK(hipStreamSynchronize(s));
-      m_valid = hb[2 * K + 1];
-      // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
-      std::vector<std::pair<uint32_t, uint64_t>> cand;
-      for (uint32_t k = 0; k < K; ++k) cand.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
-      std::sort(cand.begin(), cand.end());
-      for (auto& cb : cand)
-        if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
-      if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
-      bk.emplace_back(n_seq, m_valid);
-    }
-    if (tm) tm->mark("kb_bounds");
-    const size_t nbk = bk.size() - 1;
-    // The sort's free ping-pong buffer (m items) holds the kept (b, g) pairs of a bucket.
-    // Pipelined (default): bucket k+1 is mapped on the side stream while bucket k is applied
-    // on s, with kept pairs, marks and counters double-buffered by bucket parity — each needs
-    // half of the buffer.  The map of bucket k+1 anchors the giant at the last rank of bucket
-    // k-1 (launch_kb_map).
-    uint64_t max_e = 0;
-    for (size_t k = 0; k < nbk; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
-    const char* epp = getenv("SHEEP_KB_PIPE");
-    bool per_bucket = es && es[0] == '2';
-    const bool pipe = (epp ? atoi(epp) != 0 : true) && !per_bucket && 2 * max_e <= m;
-    const char* erf = getenv("SHEEP_KB_REFRESH");
-    const bool refresh = erf ? atoi(erf) != 0 : true;
-    uint64_t* kept[2] = {spare, pipe ? spare + m / 2 : spare};
-    auto par = [&](size_t k) { return pipe ? (int)(k & 1) : 0; };
-    auto anchor_of = [&](size_t k) -> uint32_t {
-      size_t a = pipe ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
-      return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
-    };
-    auto map_k = [&](size_t k, hipStream_t st) {
-      int p = par(k);
-      size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
-      launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
-                    kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws,
-                    bins, nb, st);
-      if (tm) tm->span_end(sp, st);
-    };
-    auto apply_k = [&](size_t k, hipStream_t st) {
-      int p = par(k);
-      launch_kb_apply(bk[k + 1].second > bk[k].second, bk[k].first, bk[k + 1].first, anchor_of(k),
-                      uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
-                      spqs + p * spq_words, counters + p * 16, pipe && refresh, stats, ws, st);
-    };
-    if (pipe) {
-      hipStream_t s2 = c.side;
-      hipEvent_t* ev_map = c.kb_ev;
-      hipEvent_t* ev_apply = c.kb_ev + 2;
-      HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
-      HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
-      map_k(0, s2);
-      HIP_CHECK(hipEventRecord(ev_map[0], s2));
-      for (size_t k = 0; k < nbk; ++k) {
-        if (k + 1 < nbk) {  // map k+1 reuses the buffers of bucket k-1: wait for its apply
-          if (k >= 1) HIP_CHECK(hipStreamWaitEvent(s2, ev_apply[(k + 1) & 1], 0));
-          map_k(k + 1, s2);
-          HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
-        }
-        HIP_CHECK(hipStreamWaitEvent(s, ev_map[k & 1], 0));
-        apply_k(k, s);
-        HIP_CHECK(hipEventRecord(ev_apply[k & 1], s));
+    launch_kb_bounds(sorted, m, K_e, K_r, n_seq, lo_bit, bounds, s);
+    std::vector<unsigned long long> hb(2 * (K + 1));
+    HIP_CHECK(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    m_valid = hb[2 * K + 1];
+    // distinct rank boundaries; bucket k = ranks [B_k, B_{k+1}), edges [e_k, e_{k+1})
+    std::vector<std::pair<uint32_t, uint64_t>> cand;
+    for (uint32_t k = 0; k < K; ++k) cand.emplace_back((uint32_t)hb[2 * k], hb[2 * k + 1]);
+    std::sort(cand.begin(), cand.end());
+    for (auto& cb : cand)
+      if (cb.first < n_seq && (bk.empty() || cb.first > bk.back().first)) bk.push_back(cb);
+    if (bk.empty() || bk[0].first != 0) bk.insert(bk.begin(), {0u, 0ull});
+    bk.emplace_back(n_seq, m_valid);
+  }
+  if (tm) tm->mark("kb_bounds");
+  const size_t nbk = bk.size() - 1;
+  // The sort's free ping-pong buffer (m items) holds the kept (b, g) pairs of a bucket.
+  // Pipelined (default): bucket k+1 is mapped on the side stream while bucket k is applied
+  // on s, with kept pairs, marks and counters double-buffered by bucket parity — each needs
+  // half of the buffer.  The map of bucket k+1 anchors the giant at the last rank of bucket
+  // k-1 (launch_kb_map).
+  uint64_t max_e = 0;
+  for (size_t k = 0; k < nbk; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
+  const bool per_bucket = knobs().tree_stats == 2;
+  const bool pipe = knobs().kb_pipe && !per_bucket && 2 * max_e <= m;
+  uint64_t* kept[2] = {spare, pipe ? spare + m / 2 : spare};
+  auto par = [&](size_t k) { return pipe ? (int)(k & 1) : 0; };
+  auto anchor_of = [&](size_t k) -> uint32_t {
+    size_t a = pipe ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
+    return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
+  };
+  // The giant bitmap's reference vertex lives in slot j & 1 for map j: the rebase before map
+  // j reads slot (j-1) & 1 and writes slot j & 1, at a point where neither stream touches the
+  // union-find (map j-1 and apply j-1 complete); an apply uses the slot most recently written
+  // on its stream.
+  if (!knobs().kb_gbits) gbits = nullptr;
+  auto rebase = [&](size_t j) {
+    if (!gbits) return;
+    launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), s);
+  };
+  auto map_k = [&](size_t k, hipStream_t st) {
+    int p = par(k);
+    size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
+    launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
+                  kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws,
+                  bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, st);
+    if (tm) tm->span_end(sp, st);
+  };
+  auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
+    int p = par(k);
+    launch_kb_apply(bk[k + 1].second > bk[k].second, bk[k].first, bk[k + 1].first, anchor_of(k),
+                    uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
+                    spqs + p * spq_words, counters + p * 16, pipe && knobs().kb_refresh, stats,
+                    ws, gbits, gbits ? gx + (slot & 1) : nullptr, st);
+  };
+  if (pipe) {
+    // map k+1 runs on the side stream while bucket k is applied; the rebase for map k+1 sits
+    // on s after map k has finished (and after apply k-1), so map k+1 waits for it
+    hipStream_t s2 = c.side;
+    hipEvent_t* ev_map = c.kb_ev;
+    hipEvent_t* ev_reb = c.kb_ev + 2;
+    HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
+    HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
+    map_k(0, s2);
+    HIP_CHECK(hipEventRecord(ev_map[0], s2));
+    size_t slot = 0;
+    for (size_t k = 0; k < nbk; ++k) {
+      HIP_CHECK(hipStreamWaitEvent(s, ev_map[k & 1], 0));
+      if (k + 1 < nbk) {
+        rebase(k + 1);
+        slot = k + 1;
+        HIP_CHECK(hipEventRecord(ev_reb[k & 1], s));
+        HIP_CHECK(hipStreamWaitEvent(s2, ev_reb[k & 1], 0));
+        map_k(k + 1, s2);
+        HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
       }
-    } else {
-      for (size_t k = 0; k < nbk; ++k) {
-        if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
-        map_k(k, s);
-        apply_k(k, s);
-        if (per_bucket) {
-          unsigned long long h[16];
-          HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
-          HIP_CHECK(hipStreamSynchronize(s));
-          fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
-                  k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[8], h[9], h[10], h[11], h[12]);
-        }
+      apply_k(k, slot, s);
+    }
+  } else {
+    for (size_t k = 0; k < nbk; ++k) {
+      if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
+      if (k >= 1) rebase(k);
+      map_k(k, s);
+      apply_k(k, k, s);
+      if (per_bucket) {
+        unsigned long long h[16];
+        HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu finds %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
+                k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]);
       }
     }
   }
@@ -481,28 +528,6 @@ static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                             bounds.begin()) - 1;
     if (i > 0 && i < nb - 1) cuts.push_back(i);
   }
-  // Percolation window: where the records below rank r reach a mean degree 2E(r)/r of about
-  // 0.25..1.5, the giant component forms inside a bucket, and with no union-find help inside
-  // the bucket the zipper's walks get long (RMAT-26: two such buckets held 4 of the 14 ms of
-  // zipper time, 19 steps per edge against ~1.05 elsewhere).  Buckets there are cut TR times
-  // finer than the rank quantiles (SHEEP_KB_TRANS, 0 = off).  E(r) is exact at bin bounds.
-  // Measured and OFF by default: the window holds far more buckets than the two slow ones
-  // (RMAT-26 95 -> 129 buckets: 77.2 -> 84.5 ms; LJ-shape 7.6 -> 9.1 ms).
-  const char* et = getenv("SHEEP_KB_TRANS");
-  const uint32_t TR = et ? (uint32_t)atoi(et) : 0;
-  if (TR > 1) {
-    const uint64_t spacing = std::max<uint64_t>(1, (uint64_t)n_seq / ((uint64_t)K_r * TR));
-    uint64_t last = ~0ull;
-    for (uint32_t i = 1; i + 1 < nb; ++i) {
-      const double r = (double)bounds[i], dens = r > 0 ? 2.0 * (double)bin_start[i] / r : 0.0;
-      if (dens < 0.25 || dens > 1.5) continue;
-      const uint64_t slot = bounds[i] / spacing;
-      if (slot != last) {
-        cuts.push_back(i);
-        last = slot;
-      }
-    }
-  }
   std::sort(cuts.begin(), cuts.end());
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
   return cuts;
@@ -534,26 +559,20 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(m) * 4);
   if (tm) tm->mark("tree_init");
-  const char* ea = getenv("SHEEP_TREE_ALGO");
-  bool kb = !(ea && strcmp(ea, "zip") == 0);
-  const char* es = getenv("SHEEP_TREE_STATS");
-  bool stats = es && (es[0] == '1' || es[0] == '2');
+  const bool stats = knobs().tree_stats != 0;
   // Sort keys: hi's bits [lo_bit, top + 1) — bit `top` puts INVALID his after every rank.
-  // kb needs hi order only down to groups of 2^lo_bit ranks (bucket ranges; wave dedupe and
-  // the run lengths that pst needs are done per group inside k_kb_map): 18 bits = 2 passes.
-  // The plain zipper only needs the top 16 bits (order affects work, never the result).
+  // kb needs hi order only down to groups of 2^lo_bit ranks (bucket ranges; the run lengths
+  // that pst needs are counted per group inside k_kb_map): 18 bits = 2 passes.
   int top = bits_for(n_seq);
-  int lo_bit = std::max(0, top + 1 - (kb ? 18 : 16));
+  int lo_bit = std::max(0, top + 1 - 18);
   // pst from degrees (di) needs the run length of every hi: counted by k_kb_map.  Otherwise
-  // (and for the plain zipper) pst_weight[lo] += 1 per record in the edge pass.
-  bool pst_count = kb && di;
+  // pst_weight[lo] += 1 per record in the edge pass.
+  bool pst_count = di != nullptr;
   // Large inputs: rank gathers in partitioned order (launch_part_gather), via items_b/items.
   bool part = use_part(m);
   const uint32_t* src = d_uv;
   // Hi bins (one scatter pass) when the degrees are at hand; else the two-pass radix sort.
-  const char* esort = getenv("SHEEP_SORT");
-  const bool use_bins = kb && pst_count && m >= (1ull << 20) && n_seq > 256 &&
-                        !(esort && strcmp(esort, "radix") == 0);
+  const bool use_bins = pst_count && m >= (1ull << 20) && n_seq > 256 && !knobs().sort_radix;
   // The bins come from the chunk degree sums (seq order): they are summed and copied to the
   // host BEFORE the second partition pass is enqueued, so the host cuts the bins while the GPU
   // runs that pass instead of idling for the round trip.
@@ -620,7 +639,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     launch_fill(hcnt, 0, n_seq, s);
   }
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
-  tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, kb, stats, ws, s, tm,
+  tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, stats, ws, s, tm,
                    use_bins ? &given : nullptr, dbins, nbins);
   if (tm) tm->mark("tree_insert");
   if (pst_count) {
@@ -631,12 +650,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     unsigned long long h[16];
     HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (kb)
-      fprintf(stderr, "tree_stats algo=kb edges=%llu kept=%llu zip_edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
-              h[0], h[5], h[8], h[9], h[10], h[11], h[12]);
-    else
-      fprintf(stderr, "tree_stats algo=zip edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
-              h[1], h[2], h[3], h[4], h[5]);
+    fprintf(stderr, "tree_stats algo=kb edges=%llu kept=%llu map_finds=%llu zip_edges=%llu steps=%llu cas=%llu casfail=%llu maxsteps=%llu\n",
+            h[0], h[5], h[7], h[8], h[9], h[10], h[11], h[12]);
   }
 }
 
@@ -662,7 +677,7 @@ static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uin
   uint64_t* spare = (sorted == items) ? items_b : items;
   if (tm) tm->mark("bucket_sort");
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
-  tree_from_sorted(c, sorted, spare, m, n, lo_bit, d_parent, jump, nullptr, true, false, ws, s, tm);
+  tree_from_sorted(c, sorted, spare, m, n, lo_bit, d_parent, jump, nullptr, false, ws, s, tm);
   if (tm) tm->mark("tree_insert");
 }
 
@@ -843,7 +858,7 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   auto ev = L.span(L.map_ev, s);
   launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
                 d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws, L.bins,
-                (uint32_t)L.bounds.size(), s);
+                (uint32_t)L.bounds.size(), nullptr, nullptr, s);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
@@ -883,7 +898,8 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   auto ev = L.span(L.apply_ev, s);
   launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
-                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, s);
+                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, nullptr,
+                  nullptr, s);
   HIP_CHECK(hipEventRecord(ev.second, s));
 }
 
@@ -960,6 +976,32 @@ int sheep_release(void) {
   if (c.ls_live > 0) throw ApiError(-EBUSY, "sheep_release: a lockstep session is live");
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.scratch.release();
+  API_END
+}
+
+int sheep_set_option(const char* name, long long value) {
+  API_BEGIN
+  if (!name) throw ApiError(-EINVAL, "null option name");
+  Knobs& k = knobs();
+  for (const KnobDef& d : kKnobs)
+    if (!strcmp(d.name, name)) {
+      k.*d.field = (int)value;
+      return SHEEP_OK;
+    }
+  throw ApiError(-EINVAL, std::string("unknown option ") + name);
+  API_END
+}
+
+int sheep_get_option(const char* name, long long* value) {
+  API_BEGIN
+  if (!name || !value) throw ApiError(-EINVAL, "null argument");
+  Knobs& k = knobs();
+  for (const KnobDef& d : kKnobs)
+    if (!strcmp(d.name, name)) {
+      *value = k.*d.field;
+      return SHEEP_OK;
+    }
+  throw ApiError(-EINVAL, std::string("unknown option ") + name);
   API_END
 }
 
@@ -1078,8 +1120,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   // the degree pass's first kernel: it runs on the side stream beside the rest of the degree
   // pass and the sequence sort (SHEEP_PART_OVERLAP=0: in line, after them; =1: after the
   // whole degree pass).
-  static const char* epo = getenv("SHEEP_PART_OVERLAP");
-  const int ov = epo ? atoi(epo) : 2;
+  const int ov = knobs().part_overlap;
   const bool overlap = ov != 0 && m > 0 && use_part(m);
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);

@@ -26,6 +26,32 @@ struct Scratch {
   void release();
 };
 
+// Tuning options.  Every setting gives the same results (the etree is unique); they move work
+// between kernels.  Read from SHEEP_<NAME> environment variables once, when the library first
+// initialises a device, and changeable afterwards through sheep_set_option (include/
+// sheep_amd.h) — never re-read per call.
+struct Knobs {
+  int degree = 0;        // SHEEP_DEGREE: 0 auto (bucketed from 2^18 records), 1 atomic, 2 bucketed
+  int edge_part = -1;    // SHEEP_EDGE_PART: partitioned rank gathers; -1 auto (m >= 2^22), 0, 1
+  int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
+                         //   after it (1), in line (0)
+  int seq_compact = 1;   // SHEEP_SEQ_COMPACT: sort only the ids with degree > 0
+  int sort_radix = 0;    // SHEEP_SORT (1 = "radix"): two radix passes instead of the hi bins
+  int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
+  int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)
+  int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
+  int kb_refresh = 1;    // SHEEP_KB_REFRESH: re-resolve the kept starts before the zipper
+  int kb_gbits = 1;      // SHEEP_KB_GBITS: giant bitmap in front of the map's union-find
+  int degb_plain = 1;    // SHEEP_DEGB_PLAIN: histogram adds without wave matching (bit 0: 64K
+                         //   buckets, bit 1: small buckets)
+  int degb_hist16 = 1;   // SHEEP_DEGB_HIST: one-read 64K-id histogram (0: two halves)
+  int bin_tm = 1;        // SHEEP_BIN_TM: tile-major count matrices
+  int bin_scatter = 1;   // SHEEP_BIN_SCATTER: unstable 16K-item bin scatter (0: stable radix scatter)
+  int ep_plain = 1;      // SHEEP_EP_PLAIN: edge pass counts bins with plain LDS atomics
+  int tree_stats = 0;    // SHEEP_TREE_STATS: 1 totals, 2 per bucket (stderr; diagnostics)
+};
+Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
+
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -122,9 +148,6 @@ void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* 
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
                            hipStream_t s,
                            const uint32_t* nsd = nullptr);
-// variant = load + 4*jump + 8*queue (see sheep_kernels.hip); ws: 8 u64 device words.
-void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
-                        int variant, bool stats, unsigned long long* ws, hipStream_t s);
 void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
                       uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s);
 // One kb bucket in two halves (sheep_kernels.hip): the map (records -> kept pairs + giant marks
@@ -135,12 +158,21 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t* bitmap, uint32_t* counters, int gshift,
                    uint32_t* cnt /* nullable: hi run lengths */, bool stats,
                    unsigned long long* st, const uint32_t* bins /* nullable: hi bins */,
-                   uint32_t nb, hipStream_t s);
+                   uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,
+                   const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
+                   hipStream_t s);
+// Before a map (nothing else touching the union-find): keep the giant bitmap's reference
+// vertex (*gx_rd) if it is in the anchor's component, else move it to the anchor and clear
+// the bitmap (n_seq / 32 + 2 words); the result goes to *gx_wr.
+void launch_gb_rebase(uint32_t* gbits, uint32_t n_seq, const uint32_t* uf, uint32_t anchor,
+                      const uint32_t* gx_rd, uint32_t* gx_wr, hipStream_t s);
 // refresh: re-resolve the kept starts against the current union-find first (pipelined loop).
+// gbits / gx: the giant bitmap and the slot written by the latest rebase on this stream.
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
-                     bool refresh, bool stats, unsigned long long* st, hipStream_t s);
+                     bool refresh, bool stats, unsigned long long* st, uint32_t* gbits,
+                     const uint32_t* gx, hipStream_t s);
 // Lockstep exchange of one bucket (sheep_ls_*): pack this rank's mark words [w0, w1] (ms u64
 // slots) and kept pairs (padded to cap) for an all-gather; unpack P such blocks into the
 // bitmap (OR) and a contiguous kept array, setting *n_kept = P * cap.

@@ -576,10 +576,7 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 // bit 0: k_degb_hist16, bit 1: k_degb_hist.  The small-bucket histogram keeps the matching:
 // RMAT-22's 4096-id buckets repeat hub ids within a wave (degree 0.88 -> 0.94 ms plain), the
 // LJ shape gains (0.81 -> 0.72 ms).
-static int degb_plain() {
-  static const char* e = getenv("SHEEP_DEGB_PLAIN");
-  return e ? atoi(e) : 1;
-}
+static int degb_plain() { return knobs().degb_plain; }
 
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
@@ -630,8 +627,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
                      nchunks, ep, selfc, tm);
-  const char* eh = getenv("SHEEP_DEGB_HIST");
-  if (H > 1 && !(eh && atoi(eh) == 0))
+  if (H > 1 && knobs().degb_hist16)
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
                        (const unsigned long long*)bstart, stats, degb_plain() & 1);
@@ -951,10 +947,7 @@ k_bin_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint6
 }
 
 // SHEEP_BIN_TM=0: the digit-major counts and one flat scan (the previous layout).
-static bool bin_tile_major() {
-  static const char* e = getenv("SHEEP_BIN_TM");
-  return e ? atoi(e) != 0 : true;
-}
+static bool bin_tile_major() { return knobs().bin_tm != 0; }
 
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
                   uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
@@ -972,8 +965,7 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
     if (n == 0) return;
     tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
     publish();
-    static const char* ebs = getenv("SHEEP_BIN_SCATTER");  // 0: the stable 8192-item scatter
-    if (!ebs || atoi(ebs) != 0) {
+    if (knobs().bin_scatter) {  // 0: the stable 8192-item scatter
       hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,
                          in, out, n, (const uint32_t*)counts, digits);
       return;
@@ -1345,8 +1337,7 @@ void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank,
   if (!tm && nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
   auto k = tm ? (pre ? k_edge_pass_tiles<9, true, true, true> : k_edge_pass_tiles<9, false, true, true>)
               : (pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>);
-  static const char* epl = getenv("SHEEP_EP_PLAIN");  // bin counts by plain LDS atomics
-  const int plain = epl ? atoi(epl) : 1;
+  const int plain = knobs().ep_plain;  // bin counts by plain LDS atomics
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
                      (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits, plain);
 }
@@ -1700,29 +1691,7 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, uint64_t 
   atomicMax(&stats[4], (unsigned long long)maxsteps);
 }
 
-// Variant A: one edge per thread per iteration, grid-stride (a wave waits for its slowest lane).
-template <int LOAD, int JUMP, bool STATS>
-__global__ void k_tree_loop(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
-                            uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
-  ZCount c;
-  uint64_t edges = 0;
-  uint32_t maxsteps = 0;
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint64_t it = items[i];
-    uint32_t b = (uint32_t)(it >> 32);
-    if (b == INV) continue;
-    ZState s;
-    zstart(s, (uint32_t)it, b);
-    uint32_t st0 = c.steps;
-    while (!zip_step<LOAD, JUMP, STATS>(parent, jump, s, c)) {
-    }
-    if (STATS) { edges++; maxsteps = max(maxsteps, c.steps - st0); }
-  }
-  flush_stats<STATS>(stats, edges, c, maxsteps);
-}
-
-// Variant B: lane-level work queue.  Each wave pulls chunks of edges in increasing order and
+// Lane-level work queue.  Each wave pulls chunks of edges in increasing order and
 // every lane that finishes an edge takes the next one at the following step, so a wave never
 // idles behind its slowest lane.
 // Edge source of the queue: packed u64 items (hi << 32 | lo), or (kb) the spine queue
@@ -1801,41 +1770,6 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
   flush_stats<STATS>(stats, edges, c, maxsteps);
 }
 
-template <int LOAD, int JUMP, bool STATS>
-__global__ void k_tree_queue(const uint64_t* __restrict__ items, uint64_t n, uint32_t* parent,
-                             uint32_t* jump, unsigned long long* next, unsigned long long* stats) {
-  (void)next;
-  EdgeSrc src{items};
-  tree_queue_body<LOAD, JUMP, STATS, false>(src, n, parent, jump, stats, ZRec());
-}
-
-
-typedef void (*TreeKernel)(const uint64_t*, uint64_t, uint32_t*, uint32_t*, unsigned long long*,
-                           unsigned long long*);
-
-template <int LOAD, int JUMP, bool STATS>
-static TreeKernel pick_tree(int queue) {
-  return queue ? k_tree_queue<LOAD, JUMP, STATS> : k_tree_loop<LOAD, JUMP, STATS>;
-}
-
-template <bool STATS>
-static TreeKernel pick_tree(int load, int jmp, int queue) {
-  if (load == 0) return jmp ? pick_tree<0, 1, STATS>(queue) : pick_tree<0, 0, STATS>(queue);
-  if (load == 1) return jmp ? pick_tree<1, 1, STATS>(queue) : pick_tree<1, 0, STATS>(queue);
-  return jmp ? pick_tree<2, 1, STATS>(queue) : pick_tree<2, 0, STATS>(queue);
-}
-
-// variant = load + 4 * jump + 8 * queue; ws = 8 u64 words of device scratch (counter + stats).
-void launch_tree_insert(const uint64_t* items, uint64_t n, uint32_t* parent, uint32_t* jump,
-                        int variant, bool stats, unsigned long long* ws, hipStream_t s) {
-  if (n == 0) return;
-  int load = variant & 3, jmp = (variant >> 2) & 1, queue = (variant >> 3) & 1;
-  TreeKernel k = stats ? pick_tree<true>(load, jmp, queue) : pick_tree<false>(load, jmp, queue);
-  (void)hipMemsetAsync(ws, 0, 8 * sizeof(unsigned long long), s);
-  unsigned grid = queue ? (unsigned)MAX_GRID : grid_for(n);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, items, n, parent, jump, ws, ws + 1);
-}
-
 __device__ void zip_insert(uint32_t* parent, uint32_t* jump, uint32_t a, uint32_t b) {
   ZState s;
   ZCount c;
@@ -1905,6 +1839,16 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, u
 //   g == G (the giant, see SpineInfo): b is marked in the bucket's rank bitmap;
 //   otherwise (g, b) is kept for the zipper;
 //   cnt[b] += 1 (nullable: the run length of b that pst needs).
+// Giant membership without the union-find: gbits (nullable) holds one bit per rank, set only
+// for ranks known to lie in the component of the reference vertex X = *gx; the rebase before
+// this launch (k_gb_rebase) made X a member of the anchor's component, so a set bit means
+// g = G with no find at all.  Only the other records (non-giant components, and giant members
+// whose bit is not set yet) run the find, and those finds are batched: every lane first loads
+// its KM_R records and their bitmap words, then walks all of its misses' chains together (the
+// loads of different records interleave), and a miss that reaches the giant sets its bit for
+// the records that follow.  Bits are set by this map, by k_kb_fold (the bucket's marked ranks)
+// and by k_kb_label (the bucket's ranks that ended in X's component); they are only ever
+// cleared by k_gb_rebase when X moves to another component (before the giant has formed).
 // A block takes chunks of KM_CHUNK records; marks and counts of ranks within KM_WIN of the
 // chunk's first group go to LDS (bitmap + packed 16-bit counts) and reach global memory once
 // per word per chunk — a hub's records span many waves, and same-word atomics from every
@@ -1912,101 +1856,187 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, u
 static constexpr int KM_THREADS = 1024;
 static constexpr int KM_CHUNK = 8192;       // < 65536: the packed 16-bit counts cannot carry
 static constexpr uint32_t KM_WIN = 32768;   // ranks
+static constexpr int KM_R = KM_CHUNK / KM_THREADS;  // records per lane per chunk
+static constexpr uint32_t KM_FLUSH = 65535 / KM_CHUNK;  // chunks per window flush at most
 
 template <bool STATS>
 __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
          int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
-         uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats, int mapmode,
-         uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, int ro_find) {
+         uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
+         uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
+         const uint32_t* __restrict__ gx) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
-  constexpr int R = KM_CHUNK / KM_THREADS;  // rounds per wave per chunk
+  __shared__ uint32_t sbins[512];
+  constexpr int R = KM_R;
   // RG: the giant's union-find root, found from the anchor rank (see launch_kb_map); it does
-  // not move while this map runs (k_kb_union links everything else below it).  G: its
-  // elimination-tree root.  Membership is tested on the root, not on the label, which the
-  // apply of the previous bucket may be rewriting meanwhile.
-  const uint32_t RG = (anchor != INV && mapmode <= 1) ? uf_find_ro(uf, anchor) : INV;
-  const uint32_t G = RG != INV ? label[RG] : INV;
+  // not move while this map runs (k_kb_union links everything else below it).  Membership is
+  // tested on the root, not on the label, which the apply of the previous bucket may be
+  // rewriting meanwhile.
+  const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  const bool use_bm = gbits != nullptr && RG != INV && *gx != INV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint64_t edges = 0, kept_n = 0, inb = 0;
-  for (uint64_t c0 = e_begin + (uint64_t)blockIdx.x * KM_CHUNK; c0 < e_end;
-       c0 += (uint64_t)gridDim.x * KM_CHUNK) {
-    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, e_end);
-    // every record of the chunk has b >= the first record's group start
-    // the chunk's records lie in [group (or bin) of its first record, that of its last)
-    const uint32_t h0 = (uint32_t)(items[c0] >> 32);
-    const uint32_t blast = (uint32_t)(items[c1 - 1] >> 32);
-    uint32_t bbase, gend;
+  uint64_t edges = 0, kept_n = 0, inb = 0, misses = 0;
+  // The LDS window starts zero and every flush re-zeroes the words it read, so a chunk never
+  // clears it; the bin bounds are searched in LDS.
+  for (uint32_t i = t; i < KM_WIN / 32; i += KM_THREADS) wbits[i] = 0;
+  if (cnt)
+    for (uint32_t i = t; i < KM_WIN / 2; i += KM_THREADS) wcnt[i] = 0;
+  if (bins)
+    for (uint32_t i = t; i < nb; i += KM_THREADS) sbins[i] = bins[i];
+  __syncthreads();
+  // Each block maps a contiguous run of chunks, so that consecutive chunks mostly share one
+  // window (a bin): the window is flushed to global memory only when the next chunk's differs,
+  // after KM_FLUSH chunks (the packed 16-bit counts must not carry), and at the end.
+  const uint64_t total = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint64_t cb = e_begin + (uint64_t)blockIdx.x * per * KM_CHUNK;
+  const uint64_t ce = min(cb + per * KM_CHUNK, e_end);
+  auto window = [&](uint32_t h0, uint32_t blast, uint32_t& bbase, uint32_t& gend) {
     if (bins) {
-      bbase = bins[bin_of(bins, nb, h0)] & ~31u;
-      gend = (uint32_t)min((uint64_t)bins[min(bin_of(bins, nb, blast) + 1, nb - 1)],
+      bbase = sbins[bin_of(sbins, nb, h0)] & ~31u;
+      gend = (uint32_t)min((uint64_t)sbins[min(bin_of(sbins, nb, blast) + 1, nb - 1)],
                            (uint64_t)bbase + KM_WIN);
       if (gend <= bbase) gend = bbase + 1;
     } else {
       bbase = ((h0 >> gshift) << gshift) & ~31u;
       gend = (uint32_t)min((((uint64_t)(blast >> gshift)) + 1) << gshift, (uint64_t)bbase + KM_WIN);
     }
+  };
+  // chunk c0's records (and its first / last hi) are loaded one chunk ahead
+  uint64_t nx[R];
+  uint32_t nh0 = 0, nbl = 0;
+  auto fetch = [&](uint64_t c0) {
+    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, ce);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t idx = c0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
+      nx[r] = idx < c1 ? items[idx] : 0ull;
+    }
+    nh0 = (uint32_t)(items[c0] >> 32);
+    nbl = (uint32_t)(items[c1 - 1] >> 32);
+  };
+  if (cb < ce) fetch(cb);
+  uint32_t since_flush = 0;
+  for (uint64_t c0 = cb; c0 < ce; c0 += KM_CHUNK) {
+    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, ce);
+    uint64_t it[R];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      it[r] = nx[r];
+      const uint64_t idx = c0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
+      vmask |= (uint32_t)(idx < c1) << r;
+    }
+    // the chunk's records lie in [group (or bin) of its first record, that of its last)
+    uint32_t bbase, gend;
+    window(nh0, nbl, bbase, gend);
     const uint32_t span = gend - bbase;  // ranks of the window that can hold records
-    for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) wbits[i] = 0;
-    if (cnt)
-      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) wcnt[i] = 0;
-    __syncthreads();
-    uint64_t out[R];  // this lane's kept pair per round (b == INVALID: none)
+    uint32_t gw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t a = (uint32_t)it[r];
+      gw[r] = (use_bm && ((vmask >> r) & 1) && a < B0) ? gbits[a >> 5] : 0u;
+    }
+    const bool more = c0 + KM_CHUNK < ce;
+    if (more) fetch(c0 + KM_CHUNK);  // issued after the bitmap loads
+    uint32_t giant = 0, miss = 0, x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t a = (uint32_t)it[r];
+      x[r] = a;
+      if (((vmask >> r) & 1) && a < B0) {
+        if ((gw[r] >> (a & 31)) & 1) giant |= 1u << r;
+        else miss |= 1u << r;
+      }
+    }
+    if (STATS) misses += (uint64_t)__popc(miss);
+    // 2. the misses' finds (path halving), all chains of the lane advanced together
+    for (uint32_t act = miss; act;) {
+      uint32_t p[R], gp[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) p[r] = ((act >> r) & 1) ? uf[x[r]] : 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (((act >> r) & 1) && p[r] == x[r]) act &= ~(1u << r);
+#pragma unroll
+      for (int r = 0; r < R; ++r) gp[r] = ((act >> r) & 1) ? uf[p[r]] : 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((act >> r) & 1) {
+          if (gp[r] == p[r]) {
+            x[r] = p[r];
+            act &= ~(1u << r);
+          } else {
+            uf[x[r]] = gp[r];  // x is a non-root forever; any ancestor is a valid pointer
+            x[r] = gp[r];
+          }
+        }
+    }
+    // 3. roots -> giant (and its bit) or the pre-bucket etree root g = label[root]
+    uint32_t lab[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (((miss >> r) & 1) && x[r] == RG) {
+        giant |= 1u << r;
+        if (use_bm) {
+          const uint32_t a = (uint32_t)it[r];
+          atomicOr(&gbits[a >> 5], 1u << (a & 31));
+        }
+      }
+      lab[r] = (((miss & ~giant) >> r) & 1) ? label[x[r]] : 0u;
+    }
     uint32_t nout = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      uint64_t idx = c0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
-      bool valid = idx < c1;
-      uint64_t it = valid ? items[idx] : ~0ull;
-      uint32_t b = (uint32_t)(it >> 32);
-      uint32_t a = valid ? (uint32_t)it : 0u;
-      uint32_t g = a;
-      if (valid && a < B0 && mapmode != 2) {
-        const uint32_t rt = ro_find ? uf_find_ro(uf, a) : uf_find<false>(uf, a);
-        g = rt == RG ? G : label[rt];
-      }
-      // dedupe (mapmode 1): keep the first lane of every distinct (g, b) in the wave.  Off by
-      // default: records are in stream order inside a group, so a wave holds ~60 distinct
-      // pairs (the loop costs more than the zipper saves); the giant's pairs, which are most
-      // of the duplicates, become bitmap marks anyway.
-      bool keep = valid;
-      uint64_t rem = mapmode == 1 ? __ballot(valid) : 0ull;
-      while (rem) {
-        int leader = __ffsll((unsigned long long)rem) - 1;
-        uint32_t lb = __builtin_amdgcn_readlane(b, leader);
-        uint32_t lg = __builtin_amdgcn_readlane(g, leader);
-        uint64_t same = __ballot(valid && b == lb && g == lg);
-        if (lane != leader && ((same >> lane) & 1)) keep = false;
-        rem &= ~same;
-      }
-      if (STATS) { edges += valid; kept_n += keep; inb += keep && a >= B0; }
+      const bool valid = (vmask >> r) & 1, gi = (giant >> r) & 1;
+      const uint32_t b = (uint32_t)(it[r] >> 32), a = (uint32_t)it[r];
+      const uint32_t g = ((miss >> r) & 1) ? lab[r] : a;
+      if (STATS) { edges += valid; kept_n += valid && !gi; inb += valid && !gi && a >= B0; }
       const uint32_t o = b - bbase;
       if (valid && cnt) {
         if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
         else atomicAdd(&cnt[b], 1u);
       }
-      bool giant = keep && g == G;
-      if (giant) {
+      if (gi) {
         if (o < span) atomicOr(&wbits[o >> 5], 1u << (o & 31));
         else atomicOr(&bitmap[b >> 5], 1u << (b & 31));
       }
-      bool k2 = keep && !giant;
-      out[r] = k2 ? (((uint64_t)b << 32) | g) : ~0ull;
+      const bool k2 = valid && !gi;
+      it[r] = k2 ? (((uint64_t)b << 32) | g) : ~0ull;
       nout += (uint32_t)__popcll(__ballot(k2));
     }
     if (lane == 0) woff[w] = nout;
+    // flush the window unless the next chunk of this block keeps it (uniform decision)
+    bool flush = !more || ++since_flush >= KM_FLUSH;
+    if (!flush) {
+      uint32_t nbase, nend;
+      window(nh0, nbl, nbase, nend);
+      flush = nbase != bbase || nend != gend;
+    }
     __syncthreads();
-    for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS)
-      if (wbits[i]) atomicOr(&bitmap[(bbase >> 5) + i], wbits[i]);
-    if (cnt)
-      for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {
-        uint32_t v = wcnt[i];
-        if (v & 0xFFFFu) atomicAdd(&cnt[bbase + 2 * i], v & 0xFFFFu);
-        if (v >> 16) atomicAdd(&cnt[bbase + 2 * i + 1], v >> 16);
+    if (flush) {
+      since_flush = 0;
+      for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) {
+        const uint32_t v = wbits[i];
+        if (v) {
+          atomicOr(&bitmap[(bbase >> 5) + i], v);
+          wbits[i] = 0;
+        }
       }
+      if (cnt)
+        for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {
+          const uint32_t v = wcnt[i];
+          if (v) {
+            if (v & 0xFFFFu) atomicAdd(&cnt[bbase + 2 * i], v & 0xFFFFu);
+            if (v >> 16) atomicAdd(&cnt[bbase + 2 * i + 1], v >> 16);
+            wcnt[i] = 0;
+          }
+        }
+    }
     // compaction: one reservation per chunk for the kept pairs of all its waves
     if (t == 0) {
       uint32_t run = 0;
@@ -2017,17 +2047,33 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
     uint32_t pos = woff[KM_THREADS / 64] + woff[w];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      uint64_t bal = __ballot(out[r] != ~0ull);
-      if (out[r] != ~0ull) kept[pos + __popcll(bal & lt)] = out[r];
+      uint64_t bal = __ballot(it[r] != ~0ull);
+      if (it[r] != ~0ull) kept[pos + __popcll(bal & lt)] = it[r];
       pos += (uint32_t)__popcll(bal);
     }
-    __syncthreads();
+    // no barrier here: the next chunk writes LDS only after its own barrier has seen every
+    // wave past this chunk's flush, and woff[w] is this wave's own slot
   }
   if (STATS) {
     atomicAdd(&stats[0], (unsigned long long)edges);
     atomicAdd(&stats[5], (unsigned long long)kept_n);
     atomicAdd(&stats[6], (unsigned long long)inb);
+    atomicAdd(&stats[7], (unsigned long long)misses);
   }
+}
+
+// Before the map of a bucket, with nothing else running on the union-find (the previous map
+// and the previous apply are complete): keep the bitmap's reference vertex X if it lies in the
+// component of this map's anchor, else move X to the anchor and clear the bitmap.  X is read
+// from one slot and written to the other (every block reads before block 0 writes).
+__global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf, uint32_t anchor,
+                            const uint32_t* __restrict__ gx_rd, uint32_t* gx_wr) {
+  const uint32_t X = *gx_rd;
+  bool keep = anchor == INV || (X != INV && uf_find_ro(uf, X) == uf_find_ro(uf, anchor));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gx_wr = anchor == INV ? INV : (keep ? X : anchor);
+  if (!keep)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x)
+      gbits[i] = 0;
 }
 
 // Star -> path for the giant.  G's edges into the bucket go to the marked ranks b1 < b2 < ...;
@@ -2131,12 +2177,18 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
 // (iota: nothing links an in-bucket rank before its bucket's union), so it is stored under
 // that component's root R directly — no find, no CAS.  k_kb_union then skips the links
 // between two marked ranks (already in one tree).
+// gbits (nullable): the marked ranks are giant members; when the bitmap's reference vertex
+// *gx lies in the anchor's component they are set there too (see k_kb_map).
 __global__ void k_kb_fold(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
-                          uint32_t* uf, uint32_t anchor) {
+                          uint32_t* uf, uint32_t anchor, uint32_t* gbits,
+                          const uint32_t* __restrict__ gx) {
   const uint32_t R = uf_find_ro(uf, anchor);
+  const uint32_t X = gbits ? *gx : INV;
+  const bool set_g = X != INV && uf_find_ro(uf, X) == R;
   for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w <= ((B1 - 1) >> 5);
        w += gridDim.x * blockDim.x) {
     uint32_t bits = word_in(bitmap, w, B0, B1);
+    if (set_g && bits) atomicOr(&gbits[w], bits);
     while (bits) {
       const uint32_t v = (w << 5) + __ffs(bits) - 1;
       bits &= bits - 1;
@@ -2179,11 +2231,33 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
 
 // counters[1] = n_linked, [2] = n_spine, [3] = n_kept are reset here for the next bucket.
 // clear_marks: the bucket's marks are cleared here (FOLD: k_kb_union read them).
+// gbits (nullable): every rank of the bucket that ended in the component of the bitmap's
+// reference vertex *gx gets its bit (one ballot-assembled word per 32 ranks).
 __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
                            uint32_t B0, uint32_t B1, uint32_t* counters, uint32_t* bitmap,
-                           int clear_marks) {
-  for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
-    if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
+                           int clear_marks, uint32_t* gbits, const uint32_t* __restrict__ gx) {
+  const uint32_t X = gbits ? *gx : INV;
+  if (X == INV) {
+    for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
+      if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
+  } else {
+    const uint32_t RX = uf_find_ro(uf, X);
+    const uint32_t v0 = B0 & ~63u;  // waves cover whole 64-rank (two-word) groups
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; v0 + (uint64_t)i < B1;
+         i += gridDim.x * blockDim.x) {
+      const uint32_t v = v0 + i;
+      bool in = false;
+      if (v >= B0) {
+        const uint32_t rt = uf_find<false>(uf, v);
+        if (parent[v] == INV) label[rt] = v;
+        in = rt == RX;
+      }
+      const uint64_t bal = __ballot(in);
+      const int lane = threadIdx.x & 63;
+      if (lane == 0 && (uint32_t)bal) atomicOr(&gbits[v >> 5], (uint32_t)bal);
+      if (lane == 32 && (uint32_t)(bal >> 32)) atomicOr(&gbits[v >> 5], (uint32_t)(bal >> 32));
+    }
+  }
   if (clear_marks)
     for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
          w += gridDim.x * blockDim.x)
@@ -2241,41 +2315,40 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
 // roots while earlier buckets are still being folded into the union-find, but both lie in the
 // anchor's component at rank B0, and an edge (a, b >= B0) may be moved to any vertex of a's
 // component at B0.  (The pipelined loop maps bucket k+1 while bucket k is applied, so it
-// anchors at the last rank of bucket k-1.)  INV: no giant (first buckets, mapmode >= 2).
-static int kb_mapmode() {
-  const char* em = getenv("SHEEP_KB_MAPMODE");
-  return em ? atoi(em) : 0;  // 0: giant spine on; 1: + wave dedupe; 2: no UF map; 3: spine off
-}
-
+// anchors at the last rank of bucket k-1.)  INV: no giant (first buckets).
+// gbits / gx (nullable): the giant bitmap and the slot of its reference vertex that
+// launch_gb_rebase wrote before this map.
 void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
-                   unsigned long long* st, const uint32_t* bins, uint32_t nb, hipStream_t s) {
-  const int mapmode = kb_mapmode();
-  if (mapmode > 1) anchor = INV;
+                   unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
+                   const uint32_t* gx, hipStream_t s) {
   if (e_end <= e_begin) return;
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
-  static const char* emg = getenv("SHEEP_KB_MGRID");  // blocks (2 per CU fit the LDS window)
-  static const uint64_t mgrid = emg ? (uint64_t)atoi(emg) : 512;
-  unsigned grid = (unsigned)std::min<uint64_t>(chunks, mgrid);
+  unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);  // 2 blocks per CU fit the LDS window
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-  static const char* ef = getenv("SHEEP_KB_MAPFIND");
-  const int ro = ef && ef[0] == 'r';
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
-                     uf, label, kept, counters + 3, bitmap, cnt, st, mapmode, anchor, bins, nb, ro);
+                     uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
+                     gx ? gbits : nullptr, gx);
+}
+
+void launch_gb_rebase(uint32_t* gbits, uint32_t n_seq, const uint32_t* uf, uint32_t anchor,
+                      const uint32_t* gx_rd, uint32_t* gx_wr, hipStream_t s) {
+  const uint32_t nwords = n_seq / 32 + 2;
+  hipLaunchKernelGGL(k_gb_rebase, dim3(std::min<uint32_t>((nwords + BLOCK - 1) / BLOCK, 1024)),
+                     dim3(BLOCK), 0, s, gbits, nwords, uf, anchor, gx_rd, gx_wr);
 }
 
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
-                     bool refresh, bool stats, unsigned long long* st, hipStream_t s) {
-  const int mapmode = kb_mapmode();
-  if (mapmode > 1) anchor = INV;
-  const char* esl = getenv("SHEEP_KB_SCAN");
-  uint32_t scan_limit = esl ? (uint32_t)atoi(esl) : 64;
+                     bool refresh, bool stats, unsigned long long* st, uint32_t* gbits,
+                     const uint32_t* gx, hipStream_t s) {
+  const uint32_t scan_limit = 64;  // spine scan: bitmap words per search
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
   uint32_t* n_kept = counters + 3;
+  if (!gx) gbits = nullptr;
   if (nonempty) {
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
@@ -2284,29 +2357,26 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
-    const char* eq = getenv("SHEEP_KB_QCHUNK");
-    const char* eg = getenv("SHEEP_KB_ZGRID");
-    uint32_t qchunk = eq ? (uint32_t)atoi(eq) : 64;
-    unsigned zgrid = eg ? (unsigned)atoi(eg) : MAX_GRID;
-    hipLaunchKernelGGL(zk, dim3(zgrid), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
+    const uint32_t qchunk = 64;  // zipper queue: edges per wave refill
+    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
                        anchor, scan_limit, qchunk);
   }
   // giant fold: the marks are relative to the anchor's component; its root R_a may later be
   // linked below the union's R (pipelined: different anchors) — the folded ranks follow it
-  static const char* ef = getenv("SHEEP_KB_FOLD");
-  const bool fold = (ef ? atoi(ef) != 0 : true) && nonempty && anchor != INV && B1 > B0;
+  const bool fold = nonempty && anchor != INV && B1 > B0;
   if (fold)
     hipLaunchKernelGGL(k_kb_fold, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
-                       0, s, (const uint32_t*)bitmap, B0, B1, uf, anchor);
+                       0, s, (const uint32_t*)bitmap, B0, B1, uf, anchor, gbits, gx);
   unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
   auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
   hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,
                      B0 > 0 ? B0 - 1 : INV);
-  hipLaunchKernelGGL(k_kb_label, dim3(grid_for(B1 - B0)), dim3(BLOCK), 0, s,
-                     (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold);
+  hipLaunchKernelGGL(k_kb_label, dim3(grid_for((uint64_t)(B1 - B0) + 64)), dim3(BLOCK), 0, s,
+                     (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold,
+                     gbits, gx);
 }
 
 // ---- lockstep exchange (multi-GPU kb loop, sheep_ls_*) -----------------------------------

@@ -38,3 +38,18 @@ def gpu():
     capi.lib()
     capi.call("sheep_gpu_init", 0)
     return capi
+
+
+@pytest.fixture
+def options(gpu):
+    """Set libsheep_amd tuning options (sheep_set_option) for one test; restored afterwards."""
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            old = gpu.set_option(k, v)
+            saved.setdefault(k, old)
+
+    yield set_
+    for k, v in saved.items():
+        gpu.set_option(k, v)

@@ -46,3 +46,14 @@ def test_lockstep_entry_points_reject_null_handles_without_gpu():
     assert L.sheep_ls_plan(None, counts, ctypes.byref(n), ctypes.byref(n)) == -errno.EINVAL
     assert b"null" in L.sheep_last_error()
     assert L.sheep_ls_free(None) == 0
+
+
+def test_options_read_once_and_settable_without_gpu():
+    """Tuning options: defaults from SHEEP_<NAME> once, then only sheep_set_option changes them;
+    unknown names are refused."""
+    import pytest
+
+    old = capi.set_option("kb_buckets", 7)
+    assert capi.set_option("kb_buckets", old) == 7
+    with pytest.raises(capi.SheepError):
+        capi.set_option("no_such_option", 1)

@@ -83,10 +83,12 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
 @pytest.mark.parametrize("scale,seed,mode,env", [
     (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
     (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
-    (16, 23, 0, {"SHEEP_EDGE_PART": "1"}),  # the partitioned gathers at a small size
-    (16, 24, 0, {"SHEEP_EDGE_PART": "0"}),  # direct gathers, hi bins
+    (16, 23, 0, {"edge_part": 1}),  # the partitioned gathers at a small size
+    (16, 24, 0, {"edge_part": 0}),  # direct gathers, hi bins
+    (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
+    (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
 ])
-def test_graph2tree_dev_front_half(oracle, gpu, monkeypatch, scale, seed, mode, env):
+def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
     and the first partition pass runs beside the degree pass and the sequence sort, with the
     compacted sequence sort, tile-major bin counts and the unstable bin scatter: seq, parent
@@ -94,8 +96,7 @@ def test_graph2tree_dev_front_half(oracle, gpu, monkeypatch, scale, seed, mode, 
     import torch
     from sheep_amd import device
 
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    options(**env)
     uv_d = device.rmat(scale, 16, seed)
     uv = uv_d.cpu().numpy().view(np.uint32)
     seq = oracle.degree_sequence(uv, mode)
@@ -220,10 +221,10 @@ def test_tre_roundtrip(api, hep_edges, tmp_path):
 
 @pytest.mark.parametrize("path", ["atomic", "bucketed"])
 @pytest.mark.parametrize("seed", range(3))
-def test_degree_paths_agree(oracle, api, monkeypatch, path, seed):
+def test_degree_paths_agree(oracle, api, options, path, seed):
     """Both degree kernels (global atomics / LDS-bucketed) on multigraphs with self-loops,
     in both degree conventions, including tiny id spaces (one id per bucket)."""
-    monkeypatch.setenv("SHEEP_DEGREE", path)
+    options(degree={"atomic": 1, "bucketed": 2}[path])
     rng = np.random.default_rng(200 + seed)
     n = [3, 5000, 70000][seed]
     m = [50, 300000, 600000][seed]
@@ -308,29 +309,24 @@ def test_merge_forests_equals_whole(oracle, gpu, P):
 
 
 KB_KNOBS = [
-    {},                                                    # defaults (giant spine on)
-    {"SHEEP_KB_MAPMODE": "1"},                             # spine + wave dedupe
-    {"SHEEP_KB_MAPMODE": "2"},                             # no union-find map (walk from a)
-    {"SHEEP_KB_MAPMODE": "3"},                             # spine off
-    {"SHEEP_KB_SCAN": "1"},                                # runs cut at every gap > 1 word
-    {"SHEEP_KB_SCAN": "0", "SHEEP_KB_BUCKETS": "256"},     # every word its own run
-    {"SHEEP_KB_BUCKETS": "4", "SHEEP_KB_RANKB": "8"},      # few, wide buckets
-    {"SHEEP_KB_BUCKETS": "512", "SHEEP_KB_QCHUNK": "1"},   # many buckets, tiny queue chunks
-    {"SHEEP_TREE_ALGO": "zip"},                            # plain zipper, no buckets
-    {"SHEEP_KB_PIPE": "0"},                                # one stream, map of bucket k after apply of k-1
-    {"SHEEP_KB_REFRESH": "0"},                             # pipelined, stale kept starts zipped as they are
-    {"SHEEP_SORT": "radix"},                               # two 9-bit radix passes instead of hi bins
-    {"SHEEP_KB_PIPE": "1", "SHEEP_KB_BUCKETS": "512", "SHEEP_KB_RANKB": "512"},  # many narrow buckets
+    {},                                              # defaults (giant bitmap + spine)
+    {"kb_gbits": 0},                                 # the map finds every record's root
+    {"kb_buckets": 4, "kb_rankb": 8},                # few, wide buckets
+    {"kb_buckets": 512},                             # many buckets
+    {"kb_pipe": 0},                                  # one stream, map of bucket k after apply of k-1
+    {"kb_pipe": 0, "kb_gbits": 0},
+    {"kb_refresh": 0},                               # pipelined, stale kept starts zipped as they are
+    {"sort": 1},                                     # two 9-bit radix passes instead of hi bins
+    {"kb_pipe": 1, "kb_buckets": 512, "kb_rankb": 512},  # many narrow buckets
 ]
 
 
-@pytest.mark.parametrize("knobs", KB_KNOBS, ids=lambda k: ",".join("%s=%s" % (a[6:], b) for a, b in k.items()) or "default")
+@pytest.mark.parametrize("knobs", KB_KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()) or "default")
 @pytest.mark.parametrize("scale,seed", [(15, 5), (17, 6)])
-def test_tree_knobs_exact(oracle, api, monkeypatch, knobs, scale, seed):
-    """The tree is the same unique etree under every bucketing / spine / queue setting: the
+def test_tree_knobs_exact(oracle, api, options, knobs, scale, seed):
+    """The tree is the same unique etree under every bucketing / bitmap / queue setting: the
     knobs change the work, never the result (R-MAT, where a giant component forms)."""
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
+    options(**knobs)
     uv = oracle.rmat(scale, 16, seed)
     seq = oracle.degree_sequence(uv)
     check_tree(oracle, api, uv, seq)
@@ -401,7 +397,7 @@ def test_evaluate_rejects_missing_part(api):
 
 
 @pytest.mark.parametrize("hist", ["1", "0"])
-def test_degree_64k_id_buckets(oracle, api, monkeypatch, hist):
+def test_degree_64k_id_buckets(oracle, api, options, hist):
     """Id spaces above 2^25 use buckets of 65536 ids: the one-read histogram with u16 LDS
     counters in segments of <= 65535 entries (hist=1) and the two-half one (hist=0) give the
     checker's degrees — with a hub repeated more than 65535 times in one bucket, so counts
@@ -409,8 +405,7 @@ def test_degree_64k_id_buckets(oracle, api, monkeypatch, hist):
     import torch
     from sheep_amd import capi, device
 
-    monkeypatch.setenv("SHEEP_DEGB_HIST", hist)
-    monkeypatch.setenv("SHEEP_DEGREE", "bucketed")
+    options(degb_hist=int(hist), degree=2)
     rng = np.random.default_rng(7)
     n_ids = (1 << 26) + 5
     m = 1 << 20
@@ -427,3 +422,24 @@ def test_degree_64k_id_buckets(oracle, api, monkeypatch, hist):
         want = oracle.degree(uv, mode, n_ids)
         assert np.array_equal(got, want)
         assert got[(3 << 16) + 17] > 65535
+
+
+def test_graph2tree_all_self_loops_many_ids(oracle, gpu):
+    """2^20 self-loop records over 200 000 ids (the hi-bin path with no estimated records):
+    every vertex is an isolated root with pst 0; the bin cut must stay within its 512 slots."""
+    import torch
+    from sheep_amd import device
+
+    m, n_ids = 1 << 20, 200000
+    ids = np.random.default_rng(5).integers(0, n_ids, m).astype(np.uint32)
+    uv = np.stack([ids, ids], axis=1)
+    s_d, p_d, w_d, n = device.graph2tree(torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32),
+                                         n_ids)
+    torch.cuda.synchronize()
+    seq = oracle.degree_sequence(uv)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == seq.size
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+    assert (p == 0xFFFFFFFF).all() and (w == 0).all()
