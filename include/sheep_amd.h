@@ -176,6 +176,47 @@ int sheep_ls_finish(void* handle, const uint32_t* d_seq, const uint32_t* d_deg,
                     void* stream);
 int sheep_ls_free(void* handle);
 
+/* ---- multi-GPU graph2tree -i -r over RCCL (graph2tree.cpp:134-201) ------------------------
+ * One process per GPU.  The communicator replaces MPI_Init / MPI_COMM_WORLD
+ * (graph2tree.cpp:134-143): rank 0 makes an id, the caller hands its 128 bytes to every rank
+ * (a file, a socket, torch.distributed: the library does not care), and every rank joins with
+ * sheep_comm_init on its current device.  The collective calls below must then be made by
+ * every rank, in the same order; a failing rank leaves the others waiting, as with MPI. */
+#define SHEEP_COMM_ID_BYTES 128
+int sheep_comm_unique_id(uint8_t* id_out);
+int sheep_comm_init(const uint8_t* id, int n_ranks, int rank);
+int sheep_comm_free(void);
+int sheep_comm_info(int* rank, int* n_ranks);
+
+/* mpiSequence (sequence.h:65-93): this rank's records (host), the id spaces MAX-reduced
+ * (:72), the degrees SUM-reduced (:78), then the same degree sequence on every rank.  seq_out
+ * holds seq_cap ids; -ERANGE (with *n_seq_out set) if the sequence is longer. */
+int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                       uint32_t* seq_out, uint32_t seq_cap, uint32_t* n_seq_out);
+
+/* JTree over this rank's records + JNodeTable::mpi_merge (jtree.h:111-136, jnode.cpp:213-250):
+ * the elimination tree of the UNION of every rank's records under seq (the same seq on every
+ * rank, e.g. from sheep_mpi_sequence).  Every rank receives the whole tree (parent) and the
+ * summed pst_weight (n_seq entries each); rank 0's is what graph2tree -r saves. */
+int sheep_build_tree_multi(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq,
+                           uint32_t n_seq, uint32_t* parent_out, uint32_t* pst_out);
+
+/* The whole graph2tree -i -r on device memory: this rank's m records (d_uv), ids < n_ids (the
+ * global id space, the same on every rank) -> seq (n_ids entries), parent and pst (n_ids
+ * entries, n_seq used) on every rank.  No partial trees: the ranks walk one bucketed tree
+ * build together, each mapping its own records and applying the kept pairs of all
+ * (DESIGN.md §6).  Synchronises the stream. */
+int sheep_graph2tree_multi_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                               uint32_t* d_seq, uint32_t* d_parent, uint32_t* d_pst,
+                               uint32_t* n_seq_out, void* stream);
+
+/* The same driver for n_ranks shards held by ONE process on the current device, one thread
+ * per rank, the collectives done as device copies (the one-device rehearsal of the P-GPU path;
+ * tests).  Rank 0's seq/parent/pst are returned; -EIO if any rank's replica differs. */
+int sheep_graph2tree_multi_local(const uint32_t* const* d_uv, const uint64_t* m, uint32_t n_ranks,
+                                 uint32_t n_ids, int degree_mode, uint32_t* d_seq,
+                                 uint32_t* d_parent, uint32_t* d_pst, uint32_t* n_seq_out);
+
 /* Partition quality of a k-way vertex partition (Partition::evaluate(graph) and
  * evaluate(graph, seq), partition.cpp:428-521) over the m edge records in HBM, counted on
  * LLAMA's undirected adjacency as the reference does.  d_parts: n_ids int16 parts (every id

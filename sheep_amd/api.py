@@ -193,3 +193,31 @@ def partition(tree, seq, ks, balance=1.03):
     capi.call("sheep_partition", _ptr(tree.parent), _ptr(tree.pst), tree.size(), _ptr(seq),
               _ptr(ks), ks.size, float(balance), _ptr(parts), n_vid, _ptr(created))
     return [parts[i, :n_vid] for i in range(ks.size)], [int(c) for c in created]
+
+
+# ---- multi-rank (graph2tree -i -r; a communicator from sheep_comm_init on every rank) ---------
+
+def mpi_sequence(uv, n_ids=0, mode=DEGREE_LLAMA):
+    """mpiSequence (sequence.h:65-93): this rank's records; the same sequence on every rank."""
+    uv = _as_edges(uv)
+    # n_ids: the id space of the whole graph (as getMaxVid, the same on every rank); the
+    # sequence cannot be longer
+    cap = max(int(n_ids), int(uv.max()) + 1 if uv.size else 0, 1)
+    seq = np.zeros(cap, np.uint32)
+    n = ctypes.c_uint32(0)
+    capi.call("sheep_mpi_sequence", _ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
+              ctypes.byref(n))
+    return seq[:n.value]
+
+
+def build_tree_multi(uv, seq):
+    """JTree on this rank's records + mpi_merge: the whole tree, on every rank."""
+    uv = _as_edges(uv)
+    seq = np.ascontiguousarray(seq, np.uint32)
+    n = seq.size
+    parent = np.zeros(max(n, 1), np.uint32)
+    pst = np.zeros(max(n, 1), np.uint32)
+    if n:
+        capi.call("sheep_build_tree_multi", _ptr(uv), uv.shape[0], _ptr(seq), n, _ptr(parent),
+                  _ptr(pst))
+    return JNodeTable(parent[:n], pst[:n])

@@ -83,6 +83,16 @@ def lib():
         "sheep_ls_apply": [vp, c.c_uint32, vp, c.c_uint32, c.c_uint32, vp],
         "sheep_ls_finish": [vp, u32p, u32p, u32p, c.c_int, u32p, u32p, vp],
         "sheep_ls_free": [vp],
+        "sheep_comm_unique_id": [vp],
+        "sheep_comm_init": [vp, c.c_int, c.c_int],
+        "sheep_comm_free": [],
+        "sheep_comm_info": [vp, vp],
+        "sheep_mpi_sequence": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, c.c_uint32, u32p],
+        "sheep_build_tree_multi": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, u32p],
+        "sheep_graph2tree_multi_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, u32p,
+                                       u32p, vp],
+        "sheep_graph2tree_multi_local": [vp, vp, c.c_uint32, c.c_uint32, c.c_int, u32p, u32p, u32p,
+                                         u32p],
         "sheep_set_option": [c.c_char_p, c.c_longlong],
         "sheep_get_option": [c.c_char_p, c.c_void_p],
         "sheep_partition": [u32p, u32p, c.c_uint32, u32p, vp, c.c_uint32, c.c_double, vp,

@@ -10,12 +10,14 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <tuple>
 #include <vector>
 
 #include "../../include/sheep_amd.h"
+#include "sheep_comm.h"
 #include "sheep_internal.h"
 
 namespace sheep {
@@ -112,13 +114,9 @@ void Scratch::release() {
   slots.clear();
 }
 
-static Ctx& init_ctx(int device) {
-  if (device < 0 || device >= 64) throw ApiError(-EINVAL, "device index out of range");
-  std::lock_guard<std::mutex> lk(g_mu);
-  Ctx& c = g_ctx[device];
-  (void)knobs();  // the environment is read once, here
-  HIP_CHECK(hipSetDevice(device));
-  if (c.device < 0) {
+// Streams, events and pinned words of a context (a device's, or a rehearsal rank thread's).
+static void ctx_setup(Ctx& c, int device) {
+  {
     HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     for (auto& e : c.kb_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -130,6 +128,28 @@ static Ctx& init_ctx(int device) {
     HIP_CHECK(hipHostMalloc(&c.h_pinned, 64, hipHostMallocDefault));
     c.device = device;
   }
+}
+
+static void ctx_teardown(Ctx& c) {
+  c.scratch.release();
+  (void)hipStreamDestroy(c.stream);
+  (void)hipStreamDestroy(c.side);
+  for (auto& e : c.kb_ev) (void)hipEventDestroy(e);
+  for (auto& e : c.part_ev) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c.bins_ev);
+  (void)hipHostFree(c.h_bstart);
+  if (c.h_chunks) (void)hipHostFree(c.h_chunks);
+  (void)hipFree(c.d_err);
+  (void)hipHostFree(c.h_pinned);
+}
+
+static Ctx& init_ctx(int device) {
+  if (device < 0 || device >= 64) throw ApiError(-EINVAL, "device index out of range");
+  std::lock_guard<std::mutex> lk(g_mu);
+  Ctx& c = g_ctx[device];
+  (void)knobs();  // the environment is read once, here
+  HIP_CHECK(hipSetDevice(device));
+  if (c.device < 0) ctx_setup(c, device);
   g_device = device;
   return c;
 }
@@ -921,11 +941,119 @@ static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t
       t += ms;
     }
     c.timings.emplace_back(name, t);
-    c.span_names.push_back(std::string(name) + "#");
-    c.timings.emplace_back(c.span_names.back().c_str(), (double)v.size());
+    c.timings.emplace_back(name == std::string("kb_map") ? "kb_map#" : "kb_apply#", (double)v.size());
   };
   sum("kb_map", L.map_ev);
   sum("kb_apply", L.apply_ev);
+}
+
+// ---- graph2tree -i -r on one rank (the multi-GPU driver) ------------------------------------
+// This rank's shard -> its degrees, summed over the ranks (mpiSequence's MPI_Allreduce,
+// sequence.h:72-78) -> the identical seq / rank on every rank -> the lockstep tree over all
+// shards (every rank maps its own records per bucket; the kept pairs and marks of all ranks are
+// all-gathered and applied by every rank) -> pst_weight summed (the merge adds the partial
+// trees' pst, jnode.cpp:174-201).  Every rank ends with seq, parent and pst.  seq_given: d_seq
+// already holds n_seq ids (sheep_build_tree_multi); else it is computed (n_ids entries).
+static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
+                           int mode, uint32_t* d_seq, bool seq_given, uint32_t n_seq_given,
+                           uint32_t* d_parent, uint32_t* d_pst, hipStream_t s, Timer* tm) {
+  require_records(m, "multi tree");
+  const size_t n = std::max<uint32_t>(n_ids, 1);
+  uint32_t* deg_local = (uint32_t*)c.scratch.get("mt_deg_local", n * 4);
+  uint32_t* selfc = (uint32_t*)c.scratch.get("mt_selfc", n * 4);
+  uint32_t* deg = (uint32_t*)c.scratch.get("mt_deg", n * 4);
+  uint32_t* rank = (uint32_t*)c.scratch.get("mt_rank", n * 4);
+  degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s);
+  if (n_ids) HIP_CHECK(hipMemcpyAsync(deg, deg_local, (size_t)n_ids * 4, hipMemcpyDeviceToDevice, s));
+  comm.allreduce_sum_u32(deg, n_ids, s);
+  if (tm) tm->mark("degree");
+  uint32_t n_seq = n_seq_given;
+  if (!seq_given) {
+    n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
+  } else {
+    launch_fill(rank, INV, n_ids, s);
+    launch_rank_scatter(d_seq, n_seq, rank, c.d_err, s);
+  }
+  check_err(c, s);
+  if (tm) tm->mark("sequence");
+  // the lockstep session keeps its buffers in this context's scratch
+  Lockstep L;
+  L.ctx = &c;
+  L.scp = &c.scratch;
+  c.ls_live++;
+  std::vector<uint64_t> counts(513, 0);
+  uint32_t nb = 0;
+  ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s);
+  check_err(c, s);
+  uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);
+  HIP_CHECK(hipMemcpyAsync(dcounts, counts.data(), (size_t)nb * 8, hipMemcpyHostToDevice, s));
+  comm.allreduce_sum_u64(dcounts, nb, s);
+  HIP_CHECK(hipMemcpyAsync(counts.data(), dcounts, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  uint32_t nbk = 0, S = 0;
+  ls_plan(L, counts.data(), &nbk, &S);
+  if (tm) tm->mark("binned");
+  // The bucket loop, pipelined: bucket k+1 is mapped and exchanged on the side stream while
+  // bucket k is applied on s.  The host waits once per bucket, for the MAX over the ranks of
+  // the kept counts (the all-gather's size).
+  const int P = comm.size();
+  hipStream_t s2 = c.side;
+  uint64_t cap_send = (uint64_t)S + std::max<uint64_t>(m, 1);
+  uint64_t* send = (uint64_t*)c.scratch.get("mt_send", cap_send * 8);
+  uint64_t* recv[2] = {nullptr, nullptr};
+  uint64_t recv_cap[2] = {0, 0};
+  int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
+  uint32_t caps[2] = {0, 0};
+  hipEvent_t* exchanged = c.kb_ev;
+  hipEvent_t* applied = c.kb_ev + 2;
+  auto produce = [&](uint32_t k) {
+    ls_map(L, k, send, (long long*)d_cnt, nullptr, s2);
+    comm.allreduce_max_i64(d_cnt, 1, s2);
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned, d_cnt, 8, hipMemcpyDeviceToHost, s2));
+    HIP_CHECK(hipStreamSynchronize(s2));
+    const uint32_t cap = (uint32_t)*(const int64_t*)c.h_pinned;
+    const uint64_t width = (uint64_t)S + cap;
+    if (width > cap_send) {  // another rank kept more pairs than this one has records
+      uint64_t* grown = nullptr;
+      HIP_CHECK(hipMalloc(&grown, width * 8));
+      HIP_CHECK(hipMemcpyAsync(grown, send, cap_send * 8, hipMemcpyDeviceToDevice, s2));
+      HIP_CHECK(hipStreamSynchronize(s2));
+      send = (uint64_t*)c.scratch.get("mt_send", width * 8);  // frees the old slot
+      HIP_CHECK(hipMemcpyAsync(send, grown, cap_send * 8, hipMemcpyDeviceToDevice, s2));
+      HIP_CHECK(hipStreamSynchronize(s2));
+      HIP_CHECK(hipFree(grown));
+      cap_send = width;
+    }
+    ls_pack(L, k, send, cap, s2);
+    const int p = k & 1;
+    if (recv_cap[p] < (uint64_t)P * width) {  // bucket k-2 (its last reader) is applied
+      recv_cap[p] = std::max<uint64_t>((uint64_t)P * width, recv_cap[p] * 5 / 4);
+      recv[p] = (uint64_t*)c.scratch.get(p ? "mt_recv1" : "mt_recv0", recv_cap[p] * 8);
+    }
+    comm.allgather_u64(send, recv[p], width, s2);
+    HIP_CHECK(hipEventRecord(exchanged[p], s2));
+    caps[p] = cap;
+  };
+  if (nbk) {
+    HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
+    HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
+    produce(0);
+    for (uint32_t k = 0; k < nbk; ++k) {
+      HIP_CHECK(hipStreamWaitEvent(s, exchanged[k & 1], 0));
+      ls_apply(L, k, recv[k & 1], (uint32_t)P, caps[k & 1], s);
+      HIP_CHECK(hipEventRecord(applied[k & 1], s));
+      if (k + 1 < nbk) {
+        if (k >= 1) HIP_CHECK(hipStreamWaitEvent(s2, applied[(k + 1) & 1], 0));
+        produce(k + 1);
+      }
+    }
+  }
+  if (tm) tm->mark("tree");
+  ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, d_pst, s);
+  comm.allreduce_sum_u32(d_pst, n_seq, s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (tm) tm->mark("pst");
+  return n_seq;
 }
 
 }  // namespace sheep
@@ -1298,6 +1426,195 @@ int sheep_ls_finish(void* handle, const uint32_t* d_seq, const uint32_t* d_deg,
 int sheep_ls_free(void* handle) {
   API_BEGIN
   delete (Lockstep*)handle;
+  API_END
+}
+
+// ---- multi-GPU: communicator + graph2tree -i -r ---------------------------------------------
+
+int sheep_comm_unique_id(uint8_t* id_out) {
+  API_BEGIN
+  if (!id_out) throw ApiError(-EINVAL, "null id");
+  rccl_unique_id(id_out);
+  API_END
+}
+
+int sheep_comm_init(const uint8_t* id, int n_ranks, int rank) {
+  API_BEGIN
+  if (!id || n_ranks < 1 || rank < 0 || rank >= n_ranks) throw ApiError(-EINVAL, "comm: id, n_ranks, rank");
+  Ctx& c = ctx();
+  if (c.comm) throw ApiError(-EBUSY, "comm: this device already has a communicator");
+  c.comm = rccl_comm(id, n_ranks, rank).release();
+  API_END
+}
+
+int sheep_comm_free(void) {
+  API_BEGIN
+  Ctx& c = ctx();
+  delete c.comm;
+  c.comm = nullptr;
+  API_END
+}
+
+int sheep_comm_info(int* rank, int* n_ranks) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!c.comm) throw ApiError(-ENOENT, "comm: no communicator (sheep_comm_init)");
+  if (rank) *rank = c.comm->rank();
+  if (n_ranks) *n_ranks = c.comm->size();
+  API_END
+}
+
+static Comm& need_comm(Ctx& c) {
+  if (!c.comm) throw ApiError(-ENOENT, "no communicator: call sheep_comm_init on every rank first");
+  return *c.comm;
+}
+
+// Timings of a multi-rank build: the phase marks, then the lockstep loop's kernel sums.
+static void multi_timings(Ctx& c, Timer& tm) {
+  std::vector<std::pair<const char*, double>> kb = c.timings;  // ls_finish's (static names)
+  tm.finish(c);
+  for (auto& x : kb) c.timings.push_back(x);
+}
+
+int sheep_graph2tree_multi_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                               uint32_t* d_seq, uint32_t* d_parent, uint32_t* d_pst,
+                               uint32_t* n_seq_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  hipStream_t s = pick(c, stream);
+  Timer tm(s);
+  uint32_t n = multi_tree(c, need_comm(c), d_uv, m, n_ids, degree_mode, d_seq, false, 0, d_parent,
+                          d_pst, s, &tm);
+  multi_timings(c, tm);
+  if (n_seq_out) *n_seq_out = n;
+  API_END
+}
+
+int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int degree_mode,
+                       uint32_t* seq_out, uint32_t seq_cap, uint32_t* n_seq_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  Comm& comm = need_comm(c);
+  hipStream_t s = c.stream;
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  // MPI_Allreduce MAX of the id spaces (sequence.h:72), then SUM of the degrees (:78)
+  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
+  int64_t* d_n = (int64_t*)c.scratch.get("mt_cnt", 8);
+  int64_t hn = n_ids;
+  HIP_CHECK(hipMemcpyAsync(d_n, &hn, 8, hipMemcpyHostToDevice, s));
+  comm.allreduce_max_i64(d_n, 1, s);
+  HIP_CHECK(hipMemcpyAsync(&hn, d_n, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  n_ids = (uint32_t)hn;
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  const size_t n = std::max<uint32_t>(n_ids, 1);
+  uint32_t* deg = (uint32_t*)c.scratch.get("deg", n * 4);
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", n * 4);
+  uint32_t* seq = (uint32_t*)c.scratch.get("h_seq", n * 4);
+  degree_dev(c, uv, m, n_ids, degree_mode, deg, nullptr, s);
+  check_err(c, s);
+  comm.allreduce_sum_u32(deg, n_ids, s);
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, seq, rank, s);
+  if (n_seq_out) *n_seq_out = n_seq;
+  if (n_seq > seq_cap) throw ApiError(-ERANGE, "mpi_sequence: seq_out holds fewer ids than the sequence");
+  if (n_seq) HIP_CHECK(hipMemcpyAsync(seq_out, seq, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  check_err(c, s);
+  API_END
+}
+
+int sheep_build_tree_multi(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq, uint32_t n_seq,
+                           uint32_t* parent_out, uint32_t* pst_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  Comm& comm = need_comm(c);
+  hipStream_t s = c.stream;
+  if (n_seq == 0) return SHEEP_OK;
+  // the index size of JTree (jtree.h:113): max(seq) + 1, the same on every rank
+  const uint32_t n_rank = *std::max_element(seq, seq + n_seq) + 1;
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_seq * 4);
+  HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
+  uint32_t* parent = (uint32_t*)c.scratch.get("h_parent", (size_t)n_seq * 4);
+  uint32_t* pst = (uint32_t*)c.scratch.get("h_pst", (size_t)n_seq * 4);
+  Timer tm(s);
+  multi_tree(c, comm, uv, m, n_rank, SHEEP_DEGREE_LLAMA, dseq, true, n_seq, parent, pst, s, &tm);
+  multi_timings(c, tm);
+  HIP_CHECK(hipMemcpyAsync(parent_out, parent, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(pst_out, pst, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  API_END
+}
+
+int sheep_graph2tree_multi_local(const uint32_t* const* d_uv, const uint64_t* m, uint32_t n_ranks,
+                                 uint32_t n_ids, int degree_mode, uint32_t* d_seq,
+                                 uint32_t* d_parent, uint32_t* d_pst, uint32_t* n_seq_out) {
+  API_BEGIN
+  if (!d_uv || !m || n_ranks == 0 || n_ranks > 64) throw ApiError(-EINVAL, "multi_local: 1..64 shards");
+  if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
+    throw ApiError(-EINVAL, "degree_mode");
+  Ctx& c0 = ctx();
+  const int dev = c0.device;
+  HIP_CHECK(hipDeviceSynchronize());
+  auto group = make_local_group((int)n_ranks);
+  const size_t n = std::max<uint32_t>(n_ids, 1);
+  std::vector<uint32_t*> outs(3 * n_ranks, nullptr);  // ranks > 0: their own seq/parent/pst
+  std::vector<uint32_t> nseq(n_ranks, 0);
+  std::vector<std::string> errs(n_ranks);
+  std::vector<int> codes(n_ranks, 0);
+  outs[0] = d_seq;
+  outs[1] = d_parent;
+  outs[2] = d_pst;
+  for (uint32_t r = 1; r < n_ranks; ++r)
+    for (int j = 0; j < 3; ++j) HIP_CHECK(hipMalloc(&outs[3 * r + j], n * 4));
+  std::vector<std::thread> th;
+  for (uint32_t r = 0; r < n_ranks; ++r)
+    th.emplace_back([&, r] {
+      Ctx c;
+      try {
+        HIP_CHECK(hipSetDevice(dev));
+        ctx_setup(c, dev);
+        std::unique_ptr<Comm> comm = local_comm(group, (int)r);
+        nseq[r] = multi_tree(c, *comm, d_uv[r], m[r], n_ids, degree_mode, outs[3 * r], false, 0,
+                             outs[3 * r + 1], outs[3 * r + 2], c.stream, nullptr);
+      } catch (const ApiError& e) {
+        errs[r] = e.what();
+        codes[r] = e.code;
+        group_abort(*group);
+      } catch (const std::exception& e) {
+        errs[r] = e.what();
+        codes[r] = -EIO;
+        group_abort(*group);
+      }
+      if (c.device >= 0) ctx_teardown(c);
+    });
+  for (auto& t : th) t.join();
+  int code = 0;
+  std::string msg;
+  for (uint32_t r = 0; r < n_ranks && !code; ++r)
+    if (codes[r] && errs[r] != "rank group aborted") { code = codes[r]; msg = errs[r]; }
+  for (uint32_t r = 0; r < n_ranks && !code; ++r)
+    if (codes[r]) { code = codes[r]; msg = errs[r]; }
+  // every replica must be the same tree (the etree is unique)
+  if (!code)
+    for (uint32_t r = 1; r < n_ranks && !code; ++r) {
+      if (nseq[r] != nseq[0]) { code = -EIO; msg = "multi_local: ranks disagree on n_seq"; break; }
+      for (int j = 0; j < 3 && !code; ++j) {
+        std::vector<uint32_t> a(nseq[0]), b(nseq[0]);
+        HIP_CHECK(hipMemcpy(a.data(), outs[j], (size_t)nseq[0] * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(b.data(), outs[3 * r + j], (size_t)nseq[0] * 4, hipMemcpyDeviceToHost));
+        if (a != b) { code = -EIO; msg = "multi_local: rank replicas diverged"; }
+      }
+    }
+  for (uint32_t r = 1; r < n_ranks; ++r)
+    for (int j = 0; j < 3; ++j) (void)hipFree(outs[3 * r + j]);
+  if (code) throw ApiError(code, msg);
+  if (n_seq_out) *n_seq_out = nseq[0];
   API_END
 }
 

@@ -1,0 +1,201 @@
+// Communicators of the multi-GPU path: RCCL over xGMI (one process per GPU), and an in-process
+// thread group that rehearses P ranks on one device.  The reference's MPI calls these replace:
+// MPI_Allreduce MAX / SUM of the degrees (sequence.h:72,78) and the MPI_Reduce of the trees
+// (jnode.cpp:241), here an all-gather of each bucket's kept pairs and a sum of pst_weight.
+#include <dlfcn.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "sheep_comm.h"
+
+namespace sheep {
+
+#define HIPC(x)                                                                                \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- RCCL, resolved at run time ------------------------------------------------------------
+struct RcclApi {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+static const RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  static std::string err;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      err = std::string("cannot load librccl.so.1: ") + dlerror();
+      return;
+    }
+    api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    api.init_rank = (decltype(api.init_rank))dlsym(h, "ncclCommInitRank");
+    api.destroy = (decltype(api.destroy))dlsym(h, "ncclCommDestroy");
+    api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
+    api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+    api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+    if (!api.get_unique_id || !api.init_rank || !api.destroy || !api.all_reduce ||
+        !api.all_gather || !api.error_string)
+      err = "librccl.so.1 lacks an entry point";
+  });
+  if (!err.empty()) throw std::runtime_error(err);
+  return api;
+}
+
+static void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string(what) + ": " + rccl().error_string(r));
+}
+
+void rccl_unique_id(uint8_t* id) {
+  ncclUniqueId u;
+  nccl_check(rccl().get_unique_id(&u), "ncclGetUniqueId");
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+struct RcclComm : Comm {
+  ncclComm_t comm = nullptr;
+  int r = 0, p = 1;
+  RcclComm(const uint8_t* id, int n_ranks, int rank) : r(rank), p(n_ranks) {
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    nccl_check(rccl().init_rank(&comm, n_ranks, u, rank), "ncclCommInitRank");
+  }
+  ~RcclComm() override {
+    if (comm) (void)rccl().destroy(comm);
+  }
+  int rank() const override { return r; }
+  int size() const override { return p; }
+  void allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+    nccl_check(rccl().all_reduce(buf, buf, n, ncclUint32, ncclSum, comm, s), "ncclAllReduce");
+  }
+  void allreduce_sum_u64(uint64_t* buf, size_t n, hipStream_t s) override {
+    nccl_check(rccl().all_reduce(buf, buf, n, ncclUint64, ncclSum, comm, s), "ncclAllReduce");
+  }
+  void allreduce_max_i64(int64_t* buf, size_t n, hipStream_t s) override {
+    nccl_check(rccl().all_reduce(buf, buf, n, ncclInt64, ncclMax, comm, s), "ncclAllReduce");
+  }
+  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override {
+    nccl_check(rccl().all_gather(send, recv, n, ncclUint64, comm, s), "ncclAllGather");
+  }
+};
+
+std::unique_ptr<Comm> rccl_comm(const uint8_t* id, int n_ranks, int rank) {
+  return std::unique_ptr<Comm>(new RcclComm(id, n_ranks, rank));
+}
+
+// ---- P threads on one device ---------------------------------------------------------------
+struct LocalGroup {
+  int P;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void*> ptrs;
+  void* staging = nullptr;  // device scratch of the reductions (grown by rank 0)
+  size_t staging_bytes = 0;
+  const void** d_ptrs = nullptr;  // device copy of ptrs
+  explicit LocalGroup(int p) : P(p), ptrs(p, nullptr) {}
+  ~LocalGroup() {
+    if (staging) (void)hipFree(staging);
+    if (d_ptrs) (void)hipFree(d_ptrs);
+  }
+  bool aborted = false;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) throw std::runtime_error("rank group aborted");
+    const uint64_t gen = generation;
+    if (++arrived == P) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen || aborted; });
+      if (aborted) throw std::runtime_error("rank group aborted");
+    }
+  }
+};
+
+void group_abort(LocalGroup& g) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.aborted = true;
+  g.cv.notify_all();
+}
+
+std::shared_ptr<LocalGroup> make_local_group(int n_ranks) {
+  return std::make_shared<LocalGroup>(n_ranks);
+}
+
+struct LocalComm : Comm {
+  std::shared_ptr<LocalGroup> g;
+  int r;
+  LocalComm(std::shared_ptr<LocalGroup> grp, int rank) : g(std::move(grp)), r(rank) {}
+  int rank() const override { return r; }
+  int size() const override { return g->P; }
+
+  // every rank publishes buf; rank 0 reduces all of them into the staging buffer; every rank
+  // copies the result back.  The barriers order the device work across the threads (each
+  // rank's stream is drained before it arrives).
+  template <typename T, typename L>
+  void reduce_all(T* buf, size_t n, hipStream_t s, L launch) {
+    HIPC(hipStreamSynchronize(s));
+    g->ptrs[r] = buf;
+    g->barrier();
+    if (r == 0) {
+      if (g->staging_bytes < n * sizeof(T)) {
+        if (g->staging) HIPC(hipFree(g->staging));
+        g->staging = nullptr;
+        HIPC(hipMalloc(&g->staging, n * sizeof(T)));
+        g->staging_bytes = n * sizeof(T);
+      }
+      if (!g->d_ptrs) HIPC(hipMalloc((void**)&g->d_ptrs, 64 * sizeof(void*)));
+      HIPC(hipMemcpyAsync((void*)g->d_ptrs, g->ptrs.data(), g->P * sizeof(void*), hipMemcpyHostToDevice, s));
+      launch((T*)g->staging, (const T* const*)g->d_ptrs, g->P, n, s);
+      HIPC(hipStreamSynchronize(s));
+    }
+    g->barrier();
+    HIPC(hipMemcpyAsync(buf, g->staging, n * sizeof(T), hipMemcpyDeviceToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    g->barrier();
+  }
+  void allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+    reduce_all(buf, n, s, launch_sum_ptrs_u32);
+  }
+  void allreduce_sum_u64(uint64_t* buf, size_t n, hipStream_t s) override {
+    reduce_all(buf, n, s, launch_sum_ptrs_u64);
+  }
+  void allreduce_max_i64(int64_t* buf, size_t n, hipStream_t s) override {
+    reduce_all(buf, n, s, launch_max_ptrs_i64);
+  }
+  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override {
+    HIPC(hipStreamSynchronize(s));
+    g->ptrs[r] = send;
+    g->barrier();
+    for (int q = 0; q < g->P; ++q)
+      if (n) HIPC(hipMemcpyAsync(recv + (size_t)q * n, g->ptrs[q], n * 8, hipMemcpyDeviceToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    g->barrier();
+  }
+};
+
+std::unique_ptr<Comm> local_comm(std::shared_ptr<LocalGroup> g, int rank) {
+  return std::unique_ptr<Comm>(new LocalComm(std::move(g), rank));
+}
+
+}  // namespace sheep

@@ -68,6 +68,7 @@ struct Ctx {
   std::vector<std::pair<const char*, double>> timings;
   std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
   int ls_live = 0;                     // live lockstep sessions (sheep_ls_*) on this device
+  struct Comm* comm = nullptr;         // this rank's communicator (sheep_comm_init), if any
 };
 
 Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)

@@ -20,6 +20,7 @@
 
 #include "powerlaw.h"
 #include "rmat.h"
+#include "sheep_comm.h"
 #include "sheep_internal.h"
 
 namespace sheep {
@@ -2459,6 +2460,26 @@ __global__ void k_forest_items(const uint32_t* __restrict__ parent, uint32_t n,
 
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_forest_items, dim3(grid_for(n)), dim3(BLOCK), 0, s, parent, n, items);
+}
+
+// ---- reductions of the in-process rank group (sheep_comm.cpp LocalComm) ---------------------
+template <typename T, bool MAX>
+__global__ void k_reduce_ptrs(T* dst, const T* const* srcs, int P, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    T v = srcs[0][i];
+    for (int q = 1; q < P; ++q) v = MAX ? (srcs[q][i] > v ? srcs[q][i] : v) : (T)(v + srcs[q][i]);
+    dst[i] = v;
+  }
+}
+
+void launch_sum_ptrs_u32(uint32_t* dst, const uint32_t* const* srcs, int P, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL((k_reduce_ptrs<uint32_t, false>), dim3(grid_for(n)), dim3(BLOCK), 0, s, dst, srcs, P, n);
+}
+void launch_sum_ptrs_u64(uint64_t* dst, const uint64_t* const* srcs, int P, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL((k_reduce_ptrs<uint64_t, false>), dim3(grid_for(n)), dim3(BLOCK), 0, s, dst, srcs, P, n);
+}
+void launch_max_ptrs_i64(int64_t* dst, const int64_t* const* srcs, int P, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL((k_reduce_ptrs<int64_t, true>), dim3(grid_for(n)), dim3(BLOCK), 0, s, dst, srcs, P, n);
 }
 
 __global__ void k_iota(uint32_t* p, uint32_t n) {

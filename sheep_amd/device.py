@@ -194,3 +194,46 @@ def graph2tree(uv, n_ids, mode=capi.DEGREE_LLAMA, seq=None, parent=None, pst=Non
     capi.call("sheep_graph2tree_dev", _p(uv), uv.shape[0], n_ids, mode, _p(seq), _p(parent),
               _p(pst), ctypes.byref(n_seq), _stream())
     return seq, parent, pst, n_seq.value
+
+
+# ---- multi-GPU (graph2tree -i -r over RCCL; include/sheep_amd.h) -------------------------------
+
+def comm_unique_id():
+    """128-byte RCCL id (rank 0 makes it; every rank passes it to comm_init)."""
+    buf = ctypes.create_string_buffer(128)
+    capi.call("sheep_comm_unique_id", ctypes.cast(buf, ctypes.c_void_p))
+    return buf.raw
+
+
+def comm_init(uid, n_ranks, rank):
+    buf = ctypes.create_string_buffer(bytes(uid), 128)
+    capi.call("sheep_comm_init", ctypes.cast(buf, ctypes.c_void_p), int(n_ranks), int(rank))
+
+
+def comm_free():
+    capi.call("sheep_comm_free")
+
+
+def graph2tree_multi(uv, n_ids, mode=capi.DEGREE_LLAMA):
+    """This rank's shard -> (seq, parent, pst, n_seq) of the whole graph, on every rank."""
+    dev = uv.device
+    out = [torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev) for _ in range(3)]
+    n_seq = ctypes.c_uint32(0)
+    capi.call("sheep_graph2tree_multi_dev", _p(uv), uv.shape[0], n_ids, mode, _p(out[0]),
+              _p(out[1]), _p(out[2]), ctypes.byref(n_seq), _stream())
+    return out[0], out[1], out[2], n_seq.value
+
+
+def graph2tree_multi_local(shards, n_ids, mode=capi.DEGREE_LLAMA):
+    """The P-rank driver with P shards on this device (one thread per rank): rank 0's result."""
+    P = len(shards)
+    dev = shards[0].device
+    ptrs = (ctypes.c_void_p * P)(*[s.data_ptr() for s in shards])
+    ms = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+    out = [torch.empty(max(n_ids, 1), dtype=torch.uint32, device=dev) for _ in range(3)]
+    n_seq = ctypes.c_uint32(0)
+    torch.cuda.synchronize()
+    capi.call("sheep_graph2tree_multi_local", ctypes.cast(ptrs, ctypes.c_void_p),
+              ctypes.cast(ms, ctypes.c_void_p), P, n_ids, mode, _p(out[0]), _p(out[1]), _p(out[2]),
+              ctypes.byref(n_seq))
+    return out[0], out[1], out[2], n_seq.value

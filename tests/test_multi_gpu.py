@@ -1,0 +1,87 @@
+"""The multi-GPU driver (graph2tree -i -r, include/sheep_amd.h sheep_graph2tree_multi_*) against
+the CPU checker, bit-exact.
+
+RCCL refuses two ranks on one device, so the P-rank driver is run as P threads of one process
+on cuda:0 (sheep_graph2tree_multi_local: the same C++ loop, its collectives as device copies),
+and the RCCL communicator itself over a one-rank group (the code path of every rank of the
+8-GPU run, collectives included)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def shards_of(uv_d, P):
+    from sheep_amd.dist import shard_bounds
+
+    m = uv_d.shape[0]
+    return [uv_d[shard_bounds(m, r, P)[0]:shard_bounds(m, r, P)[1]].contiguous() for r in range(P)]
+
+
+def check(oracle, uv, mode, seq_d, parent_d, pst_d, n):
+    seq = oracle.degree_sequence(uv, mode)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == seq.size
+    assert np.array_equal(seq_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(parent_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(pst_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+@pytest.mark.parametrize("scale,seed,P,mode", [(12, 1, 1, 0), (16, 2, 2, 0), (16, 3, 3, 1),
+                                               (18, 4, 4, 0), (18, 5, 8, 0), (19, 6, 8, 1)])
+def test_multi_local_rmat(oracle, gpu, scale, seed, P, mode):
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.rmat(scale, 16, seed)
+    torch.cuda.synchronize()
+    out = device.graph2tree_multi_local(shards_of(uv_d, P), 1 << scale, mode)
+    check(oracle, uv_d.cpu().numpy().view(np.uint32), mode, *out)
+
+
+def test_multi_local_powerlaw_and_empty_shards(oracle, gpu):
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.powerlaw(300001, 2000000, 2.3, 100.0, 11)
+    torch.cuda.synchronize()
+    sh = shards_of(uv_d, 3)
+    empty = uv_d[:0].contiguous()
+    out = device.graph2tree_multi_local([sh[0], empty, sh[1], empty, sh[2]], 300001)
+    check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
+
+
+def test_multi_local_known_answer(oracle, gpu):
+    import json
+    import os
+
+    import torch
+    from conftest import GOLDEN
+    from sheep_amd import device
+
+    ka = np.array(json.load(open(os.path.join(GOLDEN, "known_answer.json")))["records"], np.uint32)
+    uv_d = torch.from_numpy(ka.view(np.int32)).cuda().view(torch.uint32)
+    out = device.graph2tree_multi_local([uv_d[i:i + 1].contiguous() for i in range(ka.shape[0])], 7)
+    check(oracle, ka, 0, *out)
+
+
+def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
+    """The RCCL communicator path (unique id, init, the collectives) over a one-rank group:
+    graph2tree_multi_dev, mpiSequence and the JTree + mpi_merge host entry."""
+    import torch
+    from sheep_amd import api, device
+
+    uid = device.comm_unique_id()
+    device.comm_init(uid, 1, 0)
+    try:
+        uv_d = device.rmat(18, 16, 9)
+        out = device.graph2tree_multi(uv_d, 1 << 18)
+        torch.cuda.synchronize()
+        check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
+        seq = api.mpi_sequence(hep_edges, int(hep_edges.max()) + 1)
+        assert np.array_equal(seq, oracle.degree_sequence(hep_edges))
+        t = api.build_tree_multi(hep_edges, seq)
+        p, w = oracle.build_tree(hep_edges, seq)
+        assert np.array_equal(t.parent, p) and np.array_equal(t.pst, w)
+    finally:
+        device.comm_free()
