@@ -100,11 +100,13 @@ def main():
     # tensors: RCCL refuses two ranks on one device); timings are then meaningless
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--same-device", action="store_true")
-    # N > 1: lockstep (one kb loop walked by all ranks, kept pairs all-gathered per bucket) or
-    # merge (per-rank partial trees, gathered and merged on rank 0)
+    # N > 1: lockstep (the C++ driver sheep_graph2tree_multi_dev over its own RCCL communicator:
+    # one kb loop walked by all ranks, kept pairs all-gathered per bucket), lockstep-py (the
+    # same loop orchestrated from Python over torch.distributed; also the gloo / same-device
+    # rehearsal) or merge (per-rank partial trees, gathered and merged on rank 0)
     ap.add_argument("--dist", default=os.environ.get("SHEEP_DIST", "lockstep"),
-                    choices=["lockstep", "merge"])
-    # N = 1 through the N > 1 code: the lockstep loop over a one-rank process group (RCCL), to
+                    choices=["lockstep", "lockstep-py", "merge"])
+    # N = 1 through the N > 1 code: the C++ multi-rank driver over a one-rank RCCL group, to
     # measure its host overhead and collective launches on one GPU (not the default N = 1 path)
     ap.add_argument("--lockstep-1", action="store_true")
     args = ap.parse_args()
@@ -150,6 +152,18 @@ def main():
                 "generated in HBM" % (i0, gamma, args.workload))
     torch.cuda.synchronize()
     ops = DeviceOps()
+    # the C++ multi-rank driver joins its own RCCL communicator (the id travels over the torch
+    # process group); the Python orchestration rehearses it where RCCL cannot run (gloo ranks
+    # sharing one device)
+    native = (world > 1 and args.dist == "lockstep" and args.backend == "nccl"
+              and not args.same_device) or args.lockstep_1
+    if world > 1 and args.dist == "lockstep" and not native:
+        args.dist = "lockstep-py"
+    if native:
+        uid = [device.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        device.comm_init(uid[0], world, rank)
 
     def barrier():
         if world > 1:
@@ -157,11 +171,11 @@ def main():
         torch.cuda.synchronize()
 
     def step():
-        if world == 1 and args.lockstep_1:
-            return build_tree_lockstep(uv, n_ids, ops)
+        if native:
+            return device.graph2tree_multi(uv, n_ids)
         if world == 1:
             return device.graph2tree(uv, n_ids)
-        if args.dist == "lockstep":
+        if args.dist == "lockstep-py":
             return build_tree_lockstep(uv, n_ids, ops)
         return build_tree_sharded(uv, n_ids, ops)
 
@@ -242,6 +256,8 @@ def main():
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
             rec["cpu_baseline_ir"] = cpu_baseline_ir(args.cpu_scale, ef, args.cpu_scale, threads)
         print(json.dumps(rec), flush=True)
+    if native:
+        device.comm_free()
     if dist.is_initialized():
         dist.destroy_process_group()
 

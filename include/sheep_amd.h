@@ -201,6 +201,10 @@ int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int
 int sheep_build_tree_multi(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq,
                            uint32_t n_seq, uint32_t* parent_out, uint32_t* pst_out);
 
+/* JNodeTable::mpi_merge (jnode.cpp:213-250), in place on host arrays: the partial trees of all
+ * ranks (the same n jnodes, the same seq) -> etree of their union on every rank, pst summed. */
+int sheep_mpi_merge(uint32_t* parent, uint32_t* pst, uint32_t n);
+
 /* The whole graph2tree -i -r on device memory: this rank's m records (d_uv), ids < n_ids (the
  * global id space, the same on every rank) -> seq (n_ids entries), parent and pst (n_ids
  * entries, n_seq used) on every rank.  No partial trees: the ranks walk one bucketed tree

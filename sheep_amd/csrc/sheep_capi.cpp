@@ -1551,6 +1551,39 @@ int sheep_build_tree_multi(const uint32_t* edges_uv, uint64_t m, const uint32_t*
   API_END
 }
 
+int sheep_mpi_merge(uint32_t* parent, uint32_t* pst, uint32_t n) {
+  API_BEGIN
+  Ctx& c = ctx();
+  Comm& comm = need_comm(c);
+  hipStream_t s = c.stream;
+  if (n == 0) return SHEEP_OK;
+  const int P = comm.size();
+  // MPI_Reduce with the merge op (jnode.cpp:213-250): every rank's forest is gathered (as u64
+  // words, two parents each) and their union's elimination tree is built once; pst is summed.
+  const size_t words = ((size_t)n + 1) / 2;
+  uint64_t* mine = (uint64_t*)c.scratch.get("mm_mine", words * 8);
+  uint64_t* all = (uint64_t*)c.scratch.get("mm_all", (size_t)P * words * 8);
+  uint32_t* dpst = (uint32_t*)c.scratch.get("mm_pst", (size_t)n * 4);
+  uint32_t* out = (uint32_t*)c.scratch.get("mm_out", (size_t)n * 4);
+  HIP_CHECK(hipMemsetAsync(mine, 0xFF, words * 8, s));
+  HIP_CHECK(hipMemcpyAsync(mine, parent, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dpst, pst, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  comm.allgather_u64(mine, all, words, s);
+  comm.allreduce_sum_u32(dpst, n, s);
+  uint32_t* stack = (uint32_t*)c.scratch.get("mm_stack", (size_t)P * n * 4);
+  for (int r = 0; r < P; ++r)
+    HIP_CHECK(hipMemcpyAsync(stack + (size_t)r * n, (const uint32_t*)(all + (size_t)r * words),
+                             (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+  Timer tm(s);
+  merge_forests_dev(c, stack, (uint32_t)P, n, out, s, &tm);
+  check_err(c, s);
+  tm.finish(c);
+  HIP_CHECK(hipMemcpyAsync(parent, out, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(pst, dpst, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  API_END
+}
+
 int sheep_graph2tree_multi_local(const uint32_t* const* d_uv, const uint64_t* m, uint32_t n_ranks,
                                  uint32_t n_ids, int degree_mode, uint32_t* d_seq,
                                  uint32_t* d_parent, uint32_t* d_pst, uint32_t* n_seq_out) {

@@ -81,6 +81,15 @@ class JNodeTable {
     *this = JNodeTable(po, so);
   }
 
+  // mpi_merge (jnode.cpp:213-250): every rank's partial tree (same seq) -> the tree of the union
+  // of their graphs, on every rank (the reference leaves it on rank 0), pst summed.
+  void mpi_merge() {
+    std::vector<jnid_t> p = parents();
+    std::vector<esize_t> w = psts();
+    if (!p.empty()) sheep_check(sheep_mpi_merge(p.data(), w.data(), (uint32_t)p.size()), "mpi_merge");
+    *this = JNodeTable(p, w);
+  }
+
   void makeKids() {
     kid_off_.assign((size_t)end_id_ + 1, 0);
     for (jnid_t id = 0; id < end_id_; ++id)

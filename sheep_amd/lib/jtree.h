@@ -40,6 +40,24 @@ class JTree {
     build(graph, seq, opts);
     jnodes.save(filename);
   }
+  // graph2tree -i -r in one collective step (ranks of a joined ProcessGroup, comm.h): the tree
+  // of the union of every rank's partial graph under the shared seq, on every rank — the
+  // result of JTree(partial graph) + jnodes.mpi_merge() without the partial trees.
+  struct Collective {};
+  template <typename GraphType>
+  JTree(GraphType const& graph, std::vector<vid_t> const& seq, Collective, Options opts = Options()) {
+    if (!opts.isSupported())
+      throw std::invalid_argument("JTree: chordal-extension options are not built on MI355X");
+    make_index(seq);
+    std::vector<jnid_t> parent(seq.size());
+    std::vector<esize_t> pst(seq.size());
+    if (!seq.empty())
+      sheep_check(sheep_build_tree_multi(graph.records_data(), graph.records(), seq.data(),
+                                         (uint32_t)seq.size(), parent.data(), pst.data()),
+                  "JTree (collective)");
+    jnodes = JNodeTable(parent, pst);
+  }
+
   // open constructor (jtree.h:138-143)
   JTree(std::vector<vid_t> const& seq, char const* filename) : jnodes(filename) { make_index(seq); }
 

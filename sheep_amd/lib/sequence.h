@@ -32,6 +32,20 @@ std::vector<vid_t> degreeSequence(GraphType const& graph) {
   return edgeSequence(graph.records_data(), graph.records(), graph.getMaxVid(), SHEEP_DEGREE_LLAMA);
 }
 
+// mpiSequence (sequence.h:65-93): this rank's partial graph; the id spaces MAX-reduced and the
+// degrees SUM-reduced over the ranks (RCCL; a ProcessGroup from comm.h must be joined), so
+// every rank gets the same sequence.
+template <typename GraphType>
+std::vector<vid_t> mpiSequence(GraphType const& graph) {
+  std::vector<vid_t> seq(std::max<vid_t>(graph.getMaxVid(), 1));
+  uint32_t n_seq = 0;
+  sheep_check(sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
+                                 SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq),
+              "mpiSequence");
+  seq.resize(n_seq);
+  return seq;
+}
+
 // fileSequence (sequence.h:95-128): FILE degrees (degree[X]++, degree[Y]++) over the reader
 // stream, including XS1Reader's repeated last record.
 template <typename ReaderType>

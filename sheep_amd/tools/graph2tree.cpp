@@ -1,7 +1,7 @@
 // graph2tree — MI355X build of the reference CLI (graph2tree.cpp:44-243): same flags and the
 // same "Loaded graph in / Sorted in / Mapped in / Reduced in" timer lines.  The degree sort
-// and the tree build run on the GPU.  Without an MPI launcher the reference runs -i/-r as a
-// single rank; so does this binary (multi-GPU runs: python -m sheep_amd.graph2tree_dist).
+// and the tree build run on the GPU.  -i / -r run one process per GPU (the MPI ranks of the
+// reference): launch with torchrun --no-python or mpirun, see sheep_amd/lib/comm.h.
 #include <unistd.h>
 
 #include <chrono>
@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.h"
 #include "graph_wrapper.h"
 #include "jtree.h"
 #include "partition.h"
@@ -73,20 +74,26 @@ int main(int argc, char* argv[]) {
   const char* graph_filename = argv[optind];
   auto t0 = clk::now();
   std::string tmp_name;
-  if (use_mpi_sort || use_mpi_reduce) {  // one rank (graph2tree.cpp:134-157 with size 1)
-    int rank = 0;
-    part = rank + 1;
-    num_parts = 1;
-    char buf[4096];
-    if (!use_mpi_reduce && strcmp(output_filename, "") != 0) {
-      snprintf(buf, sizeof buf, "%s%02dr0.tre", output_filename, rank);
-      tmp_name = buf;
-      output_filename = tmp_name.c_str();
-    } else if (use_mpi_reduce && partitions != 0 && strcmp(output_filename, "") != 0) {
-      snprintf(buf, sizeof buf, "%s-w%04d-p", output_filename, rank);
-      tmp_name = buf;
-      output_filename = tmp_name.c_str();
+  ProcessGroup pg;
+  try {
+    if (use_mpi_sort || use_mpi_reduce) {  // graph2tree.cpp:134-157
+      pg.init();
+      part = pg.rank + 1;
+      num_parts = pg.size;
+      char buf[4096];
+      if (!use_mpi_reduce && strcmp(output_filename, "") != 0) {
+        snprintf(buf, sizeof buf, "%s%02dr0.tre", output_filename, pg.rank);
+        tmp_name = buf;
+        output_filename = tmp_name.c_str();
+      } else if (use_mpi_reduce && partitions != 0 && strcmp(output_filename, "") != 0) {
+        snprintf(buf, sizeof buf, "%s-w%04d-p", output_filename, pg.rank);
+        tmp_name = buf;
+        output_filename = tmp_name.c_str();
+      }
     }
+  } catch (const std::exception& e) {
+    fprintf(stderr, "graph2tree: %s\n", e.what());
+    return 2;
   }
   bool const is_leader = ((use_mpi_sort || use_mpi_reduce) && part == 1) ||
                          (!(use_mpi_sort || use_mpi_reduce) && strcmp(sequence_filename, "") == 0);
@@ -97,7 +104,7 @@ int main(int argc, char* argv[]) {
     auto t_load = clk::now();
     if (is_leader) printf("Loaded graph in: %f seconds\n", secs(t_load - t0));
 
-    std::vector<vid_t> seq = use_mpi_sort ? degreeSequence(graph)
+    std::vector<vid_t> seq = use_mpi_sort ? mpiSequence(graph)
                              : strcmp(sequence_filename, "") != 0 ? readSequence(sequence_filename)
                                                                   : degreeSequence(graph);
     if (use_mpi_sort && part == 1 && strcmp(sequence_filename, "") != 0) writeSequence(seq, sequence_filename);
@@ -105,16 +112,24 @@ int main(int argc, char* argv[]) {
     if (is_leader && (use_mpi_sort || strcmp(sequence_filename, "") == 0))
       printf("Sorted in: %f seconds\n", secs(t_sort - t_load));
 
+    // -i -r: the ranks build ONE tree together (no partial trees, no reduce step of its own);
+    // -r alone: partial trees, then mpi_merge, as the reference does
+    bool const collective = use_mpi_sort && use_mpi_reduce;
     bool to_file = !use_mpi_reduce && strcmp(output_filename, "") != 0 && partitions == 0;
-    JTree tree = to_file ? JTree(graph, seq, output_filename, jopts) : JTree(graph, seq, jopts);
+    JTree tree = collective ? JTree(graph, seq, JTree::Collective(), jopts)
+                 : to_file  ? JTree(graph, seq, output_filename, jopts)
+                            : JTree(graph, seq, jopts);
     auto t_map = clk::now();
     if (is_leader) printf("Mapped in: %f seconds\n", secs(t_map - t_sort));
 
-    if (use_mpi_reduce) {  // a single rank's reduce is the identity (jnode.cpp:213-250)
+    if (use_mpi_reduce) {  // jnode.cpp:213-250
+      if (!collective) tree.jnodes.mpi_merge();
       auto t_red = clk::now();
       if (is_leader) printf("Reduced in: %f seconds\n", secs(t_red - t_map));
     }
     if (partitions != 0) {
+      // every rank holds the whole tree, so each computes the same Partition (the reference
+      // partitions on rank 0 and broadcasts it, partition.cpp:69-79) and writes its own records
       tree.jnodes.makeKids();
       Partition p(seq, tree.jnodes, (part_t)partitions);
       if (strcmp(output_filename, "") != 0) p.writePartitionedGraph(graph, seq, output_filename);

@@ -123,3 +123,25 @@ def test_partition_tree_gpu_evaluation_prints_the_same(gpu, tmp_path):
     assert len(h) == 3 * 9 and d == h
     want = {r["k"]: r["ecv_down"] for r in PUB["partitions"]}
     assert [int(x) for x in re.findall(r"ECV\(down\): (\d+)", dev)] == [want[2], want[16], want[32]]
+
+
+@pytest.mark.parametrize("flags", [["-i", "-r"], ["-r"]])
+def test_graph2tree_mpi_flags_one_rank(gpu, oracle, hep_edges, tmp_path, flags):
+    """graph2tree -i -r (mpiSequence + the collective tree) and -r -s SEQ (partial tree +
+    mpi_merge) as one rank of an RCCL group (graph2tree.cpp:134-201): the saved tree equals the
+    checker's, the seq file the checker's sequence, and the reduce timer line is printed."""
+    tre = str(tmp_path / "m.tre")
+    sq = str(tmp_path / "m.seq")
+    seq = oracle.degree_sequence(hep_edges)
+    if "-i" not in flags:
+        open(sq, "w").write("".join("%d\n" % x for x in seq))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+               SHEEP_COMM_DIR=str(tmp_path), SHEEP_COMM_KEY="t")
+    out = subprocess.run([os.path.join(BIN, "graph2tree"), HEP] + flags + ["-s", sq, "-o", tre],
+                         capture_output=True, text=True, check=True, env=env).stdout
+    assert "Reduced in:" in out
+    p, s = read_tre(tre)
+    op, os_ = oracle.build_tree(hep_edges, seq)
+    assert np.array_equal(p, op) and np.array_equal(s, os_)
+    got = np.array([int(x) for x in open(sq).read().split()], np.uint32)
+    assert np.array_equal(got, seq)

@@ -6,8 +6,9 @@ GPU seconds).
 Per config, on cuda:0 through the C-ABI:
   * sheep_graph2tree_dev (degree -> sequence -> tree, LLAMA degrees): n_seq and SHA-256 of
     seq / parent / pst_weight equal the checker's (jtree.cpp:65-145 bit-exact);
-  * the 8-shard lockstep build (the 8-GPU algorithm: per-shard degrees summed, per-shard maps,
-    every shard's kept pairs applied by all) run as 8 sessions on one device: same hashes;
+  * the 8-GPU driver (per-shard degrees summed, per-shard maps, every shard's kept pairs applied
+    by all; sheep_graph2tree_multi_local = the C++ loop of sheep_graph2tree_multi_dev with its
+    collectives as device copies) with 8 rank threads on one device: same hashes;
   * sheep_partition (the product's host forwardPartition, partition.cpp:50-157) on the GPU tree
     for k = 16, 64, 256 on one table, then sheep_evaluate_dev (partition.cpp:428-521): the
     parts hash, the part count and every evaluate number (edges cut, Vcom vol, ECV(hash/down/
@@ -81,15 +82,18 @@ def test_fullsize_tree_and_partition(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", NAMES)
-def test_fullsize_lockstep_8_shards(gpu, name):
+def test_fullsize_8_ranks(gpu, name):
+    """The 8-GPU driver (sheep_graph2tree_multi_dev's loop) with 8 shards as 8 rank threads on
+    one device: the same tree as the checker's, on every rank."""
     import torch
 
-    from sheep_amd.dist import lockstep_local, shard_bounds
+    from sheep_amd import device
+    from sheep_amd.dist import shard_bounds
 
     d = DIGESTS[name]
     P = 8
     shards = [records(d, *shard_bounds(d["records"], r, P)) for r in range(P)]
-    seq_d, parent_d, pst_d, n = lockstep_local(shards, d["n_ids"])
+    seq_d, parent_d, pst_d, n = device.graph2tree_multi_local(shards, d["n_ids"])
     torch.cuda.synchronize()
     assert n == d["n_seq"]
     assert (h16(u32(seq_d, n)), h16(u32(parent_d, n)), h16(u32(pst_d, n))) == \
