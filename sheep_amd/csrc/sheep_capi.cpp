@@ -39,6 +39,7 @@ static const KnobDef kKnobs[] = {
     {"sort", &Knobs::sort_radix},         {"kb_buckets", &Knobs::kb_buckets},
     {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
     {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},
+    {"kb_defer", &Knobs::kb_defer},
     {"degb_plain", &Knobs::degb_plain},   {"degb_hist", &Knobs::degb_hist16},
     {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
@@ -419,23 +420,26 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // union-find (map j-1 and apply j-1 complete); an apply uses the slot most recently written
   // on its stream.
   if (!knobs().kb_gbits) gbits = nullptr;
+  // the map leaves its union-find misses to the apply's refresh kernel (kb_defer)
+  const bool defer = knobs().kb_defer != 0;
+  hipStream_t sa = s;  // the applies and the rebases between them
   auto rebase = [&](size_t j) {
     if (!gbits) return;
-    launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), s);
+    launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), sa);
   };
   auto map_k = [&](size_t k, hipStream_t st) {
     int p = par(k);
     size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
     launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
                   kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws,
-                  bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, st);
+                  bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer, st);
     if (tm) tm->span_end(sp, st);
   };
   auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
     int p = par(k);
     launch_kb_apply(bk[k + 1].second > bk[k].second, bk[k].first, bk[k + 1].first, anchor_of(k),
                     uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
-                    spqs + p * spq_words, counters + p * 16, pipe && knobs().kb_refresh, stats,
+                    spqs + p * spq_words, counters + p * 16, defer || (pipe && knobs().kb_refresh), stats,
                     ws, gbits, gbits ? gx + (slot & 1) : nullptr, st);
   };
   if (pipe) {
@@ -446,20 +450,25 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     hipEvent_t* ev_reb = c.kb_ev + 2;
     HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
     HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
+    if (sa != s) HIP_CHECK(hipStreamWaitEvent(sa, c.kb_ev[4], 0));
     map_k(0, s2);
     HIP_CHECK(hipEventRecord(ev_map[0], s2));
     size_t slot = 0;
     for (size_t k = 0; k < nbk; ++k) {
-      HIP_CHECK(hipStreamWaitEvent(s, ev_map[k & 1], 0));
+      HIP_CHECK(hipStreamWaitEvent(sa, ev_map[k & 1], 0));
       if (k + 1 < nbk) {
         rebase(k + 1);
         slot = k + 1;
-        HIP_CHECK(hipEventRecord(ev_reb[k & 1], s));
+        HIP_CHECK(hipEventRecord(ev_reb[k & 1], sa));
         HIP_CHECK(hipStreamWaitEvent(s2, ev_reb[k & 1], 0));
         map_k(k + 1, s2);
         HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
       }
-      apply_k(k, slot, s);
+      apply_k(k, slot, sa);
+    }
+    if (sa != s) {  // s resumes after the last apply
+      HIP_CHECK(hipEventRecord(c.kb_ev[4], sa));
+      HIP_CHECK(hipStreamWaitEvent(s, c.kb_ev[4], 0));
     }
   } else {
     for (size_t k = 0; k < nbk; ++k) {
@@ -878,7 +887,7 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   auto ev = L.span(L.map_ev, s);
   launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
                 d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws, L.bins,
-                (uint32_t)L.bounds.size(), nullptr, nullptr, s);
+                (uint32_t)L.bounds.size(), nullptr, nullptr, false, s);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {

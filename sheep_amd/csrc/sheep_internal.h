@@ -42,6 +42,7 @@ struct Knobs {
   int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
   int kb_refresh = 1;    // SHEEP_KB_REFRESH: re-resolve the kept starts before the zipper
   int kb_gbits = 1;      // SHEEP_KB_GBITS: giant bitmap in front of the map's union-find
+  int kb_defer = 1;      // SHEEP_KB_DEFER: the map's union-find misses resolved by the refresh
   int degb_plain = 1;    // SHEEP_DEGB_PLAIN: histogram adds without wave matching (bit 0: 64K
                          //   buckets, bit 1: small buckets)
   int degb_hist16 = 1;   // SHEEP_DEGB_HIST: one-read 64K-id histogram (0: two halves)
@@ -55,7 +56,7 @@ Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;     // second stream of the pipelined kb loop
+  hipStream_t side = nullptr;     // second stream of the pipelined kb loop (the maps)
   hipEvent_t kb_ev[5] = {};       // kb loop: [0,1] map done, [2,3] apply done (by parity), [4] start
   hipEvent_t part_ev[2] = {};     // graph2tree: [0] degree done, [1] first partition pass done
   hipEvent_t bins_ev = nullptr;   // the chunk degree sums reached the pinned host buffer
@@ -161,6 +162,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    unsigned long long* st, const uint32_t* bins /* nullable: hi bins */,
                    uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,
                    const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
+                   bool defer /* misses kept as (b, a) for launch_kb_apply's refresh */,
                    hipStream_t s);
 // Before a map (nothing else touching the union-find): keep the giant bitmap's reference
 // vertex (*gx_rd) if it is in the anchor's component, else move it to the anchor and clear

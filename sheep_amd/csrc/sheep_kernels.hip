@@ -1866,7 +1866,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
          int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
-         const uint32_t* __restrict__ gx) {
+         const uint32_t* __restrict__ gx, int defer) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -1955,8 +1955,9 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
       }
     }
     if (STATS) misses += (uint64_t)__popc(miss);
-    // 2. the misses' finds (path halving), all chains of the lane advanced together
-    for (uint32_t act = miss; act;) {
+    // 2. the misses' finds (path halving), all chains of the lane advanced together — unless
+    // they are deferred: then a miss is kept as (b, a) and k_kb_refresh resolves it
+    for (uint32_t act = defer ? 0u : miss; act;) {
       uint32_t p[R], gp[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) p[r] = ((act >> r) & 1) ? uf[x[r]] : 0u;
@@ -1981,14 +1982,14 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
     uint32_t lab[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if (((miss >> r) & 1) && x[r] == RG) {
+      if (!defer && ((miss >> r) & 1) && x[r] == RG) {
         giant |= 1u << r;
         if (use_bm) {
           const uint32_t a = (uint32_t)it[r];
           atomicOr(&gbits[a >> 5], 1u << (a & 31));
         }
       }
-      lab[r] = (((miss & ~giant) >> r) & 1) ? label[x[r]] : 0u;
+      lab[r] = (!defer && ((miss & ~giant) >> r) & 1) ? label[x[r]] : (uint32_t)it[r];
     }
     uint32_t nout = 0;
 #pragma unroll
@@ -2120,11 +2121,18 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 // giant becomes b's mark (tested before the atomic: most hub words are marked already) and is
 // dropped (b = INVALID, skipped by the zipper).  anchor: the map's and the spine's, so that
 // every mark of the bucket is relative to one component.
+// The map's deferred misses are kept pairs (b, a) with the raw lo a: this is where their finds
+// run (every chain of the bucket in flight at once, against the current union-find), and a
+// miss that reaches the giant sets its bit in gbits (nullable) when the bitmap's reference
+// vertex *gx lies in the anchor's component.
 __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept,
                              uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* bitmap,
-                             uint32_t B0, uint32_t anchor) {
+                             uint32_t B0, uint32_t anchor, uint32_t* gbits,
+                             const uint32_t* __restrict__ gx) {
   const uint32_t nk = *n_kept;
   const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  const uint32_t X = gbits ? *gx : INV;
+  const bool set_g = X != INV && RG != INV && uf_find_ro(uf, X) == RG;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
     const uint64_t it = kept[i];
     const uint32_t g = (uint32_t)it, b = (uint32_t)(it >> 32);
@@ -2133,6 +2141,10 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
     if (rt == RG) {
       const uint32_t bit = 1u << (b & 31);
       if (!(bitmap[b >> 5] & bit)) atomicOr(&bitmap[b >> 5], bit);
+      if (set_g) {
+        const uint32_t gb = 1u << (g & 31);
+        if (!(gbits[g >> 5] & gb)) atomicOr(&gbits[g >> 5], gb);
+      }
       kept[i] = ~0ull;
     } else {
       const uint32_t g2 = label[rt];
@@ -2323,14 +2335,14 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
-                   const uint32_t* gx, hipStream_t s) {
+                   const uint32_t* gx, bool defer, hipStream_t s) {
   if (e_end <= e_begin) return;
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);  // 2 blocks per CU fit the LDS window
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
                      uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx);
+                     gx ? gbits : nullptr, gx, (int)defer);
 }
 
 void launch_gb_rebase(uint32_t* gbits, uint32_t n_seq, const uint32_t* uf, uint32_t anchor,
@@ -2353,7 +2365,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   if (nonempty) {
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
-                         uf, (const uint32_t*)label, bitmap, B0, anchor);
+                         uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx);
     if (anchor != INV)
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);

@@ -311,6 +311,8 @@ def test_merge_forests_equals_whole(oracle, gpu, P):
 KB_KNOBS = [
     {},                                              # defaults (giant bitmap + spine)
     {"kb_gbits": 0},                                 # the map finds every record's root
+    {"kb_defer": 0},                                 # the map resolves its misses itself
+    {"kb_defer": 0, "kb_gbits": 0, "kb_pipe": 0},
     {"kb_buckets": 4, "kb_rankb": 8},                # few, wide buckets
     {"kb_buckets": 512},                             # many buckets
     {"kb_pipe": 0},                                  # one stream, map of bucket k after apply of k-1
