@@ -1562,7 +1562,7 @@ struct ZState {
 // over the forest edge (x, p) it displaced — so the redundancy rule below must not drop it
 // (only edges that have not yet changed the forest are dropped).  ZF_SPINE: the walk of the
 // current pending edge has reached the spine (checked once per pending edge).
-constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u;
+constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u, ZF_LINKED = 4u;
 
 struct ZCount {
   uint32_t steps = 0, cas = 0, fail = 0;
@@ -1632,8 +1632,11 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
         s.x = y;
       }
     }
+    // the hint and the parent are loaded together (one memory latency per step, not two);
+    // when the hint is taken the parent read is simply dropped
+    const uint32_t pj = ld_parent<LOAD>(&parent[s.x]);
     if (JUMP) {
-      uint32_t j = jump[s.x];
+      const uint32_t j = jump[s.x];
       if (j > s.x && j < s.b) {
         if (s.prev != INV) jump[s.prev] = j;
         s.prev = s.x;
@@ -1641,7 +1644,7 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
         return false;
       }
     }
-    s.p = ld_parent<LOAD>(&parent[s.x]);
+    s.p = pj;
   }
   s.fresh = false;
   if (s.p < s.b) {  // INVALID is never < b
@@ -1661,7 +1664,7 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
     return false;
   }
   if (s.p == INV) {
-    if (REC && s.x < rec.B0) rec.linked[atomicAdd(rec.n_linked, 1u)] = s.x;
+    if (REC && s.x < rec.B0) s.flags |= ZF_LINKED;  // appended by the caller, per wave
     return true;
   }
   s.a = s.b;  // zipper: continue with pending edge (b, old parent)
@@ -1763,9 +1766,21 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
       freem = __ballot(!active);
     }
     if (__ballot(active) == 0) break;
+    bool linked = false;
     if (active && zip_step<LOAD, JUMP, STATS, REC, SPINE>(parent, jump, s, c, rec, sp)) {
       active = false;
+      linked = REC && (s.flags & ZF_LINKED);
       if (STATS) maxsteps = max(maxsteps, c.steps - st0);
+    }
+    if (REC) {  // the pre-bucket roots linked in this step: one append reservation per wave
+      const uint64_t bal = __ballot(linked);
+      if (bal) {
+        const int leader = __ffsll((unsigned long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(rec.n_linked, (uint32_t)__popcll(bal));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (linked) rec.linked[base + __popcll(bal & lt)] = s.x;
+      }
     }
   }
   flush_stats<STATS>(stats, edges, c, maxsteps);
