@@ -239,6 +239,21 @@ int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
 int sheep_evaluate(const uint32_t* edges_uv, uint64_t m, const int16_t* parts, uint32_t n_parts_vid,
                    const uint32_t* seq, uint32_t n_seq, uint32_t n_parts, uint64_t* out);
 
+/* graph2tree -p K -o OUT's edge output (Partition::writePartitionedGraph, partition.cpp:588-630)
+ * on the GPU: every record (X, Y), X < Y after ordering its endpoints, self-loops skipped,
+ * assigned to the part of its lower-sequence endpoint; d_out (2m u32) receives the (X, Y)
+ * pairs grouped by part, each part in the host writer's order (X ascending, then record
+ * order); part_start (host, n_parts + 1) the first pair of each part (part_start[n_parts] = the
+ * number written).  d_parts / d_rank: n_ids int16 parts and positions in seq.  Synchronises.
+ * -ERANGE: an id outside the sequence, or an endpoint without a part in [0, n_parts). */
+int sheep_partition_edges_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                              const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts,
+                              uint32_t* d_out, uint64_t* part_start, void* stream);
+/* The same from host arrays (parts: n_parts_vid int16 per id, seq: n_seq ids), out_uv: 2m u32. */
+int sheep_partition_edges(const uint32_t* edges_uv, uint64_t m, const int16_t* parts,
+                          uint32_t n_parts_vid, const uint32_t* seq, uint32_t n_seq, uint32_t n_parts,
+                          uint32_t* out_uv, uint64_t* part_start);
+
 /* The whole single-device hot path: degree -> sequence -> tree (graph2tree's Sorted+Mapped).
  * d_seq holds n_ids entries, d_parent/d_pst hold n_ids entries (n_seq used).  Synchronises. */
 int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int degree_mode,

@@ -221,3 +221,19 @@ def build_tree_multi(uv, seq):
         capi.call("sheep_build_tree_multi", _ptr(uv), uv.shape[0], _ptr(seq), n, _ptr(parent),
                   _ptr(pst))
     return JNodeTable(parent[:n], pst[:n])
+
+
+def partition_edges(uv, parts, seq, n_parts=None):
+    """graph2tree -p K -o OUT's edge output (writePartitionedGraph, partition.cpp:588-630) on the
+    GPU: a list with, per part, the (X, Y) pairs (X < Y, self-loops skipped) in the writer's
+    order (X ascending, then record order)."""
+    uv = _as_edges(uv)
+    parts = np.ascontiguousarray(parts, np.int16)
+    seq = np.ascontiguousarray(seq, np.uint32)
+    if n_parts is None:
+        n_parts = int(parts.max()) + 1
+    out = np.zeros((max(uv.shape[0], 1), 2), np.uint32)
+    start = np.zeros(n_parts + 1, np.uint64)
+    capi.call("sheep_partition_edges", _ptr(uv), uv.shape[0], _ptr(parts), parts.size, _ptr(seq),
+              seq.size, n_parts, _ptr(out), _ptr(start))
+    return [out[int(start[p]):int(start[p + 1])] for p in range(n_parts)]

@@ -90,6 +90,10 @@ def lib():
         "sheep_mpi_sequence": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, c.c_uint32, u32p],
         "sheep_build_tree_multi": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, u32p],
         "sheep_mpi_merge": [u32p, u32p, c.c_uint32],
+        "sheep_partition_edges_dev": [u32p, c.c_uint64, vp, u32p, c.c_uint32, c.c_uint32, u32p, vp,
+                                      vp],
+        "sheep_partition_edges": [u32p, c.c_uint64, vp, c.c_uint32, u32p, c.c_uint32, c.c_uint32,
+                                  u32p, vp],
         "sheep_graph2tree_multi_dev": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, u32p, u32p,
                                        u32p, vp],
         "sheep_graph2tree_multi_local": [vp, vp, c.c_uint32, c.c_uint32, c.c_int, u32p, u32p, u32p,

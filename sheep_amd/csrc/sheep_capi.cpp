@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <thread>
 #include <stdexcept>
@@ -177,6 +178,9 @@ struct Timer {
   hipStream_t s;
   std::vector<std::pair<const char*, hipEvent_t>> ev;
   explicit Timer(hipStream_t st) : s(st) { mark("start"); }
+  // host-side durations (ms), reported after the device phases
+  std::vector<std::pair<const char*, double>> host;
+  void host_ms(const char* name, double ms) { host.emplace_back(name, ms); }
   void mark(const char* name) {
     hipEvent_t e;
     HIP_CHECK(hipEventCreate(&e));
@@ -218,6 +222,7 @@ struct Timer {
       c.span_names.push_back(std::string(x.first) + "#");
       c.timings.emplace_back(c.span_names.back().c_str(), x.second.second);
     }
+    for (auto& x : host) c.timings.push_back(x);
   }
   ~Timer() {
     for (auto& e : ev) (void)hipEventDestroy(e.second);
@@ -399,6 +404,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     bk.emplace_back(n_seq, m_valid);
   }
   if (tm) tm->mark("kb_bounds");
+  const auto host_t0 = std::chrono::steady_clock::now();
   const size_t nbk = bk.size() - 1;
   // The sort's free ping-pong buffer (m items) holds the kept (b, g) pairs of a bucket.
   // Pipelined (default): bucket k+1 is mapped on the side stream while bucket k is applied
@@ -470,6 +476,9 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       HIP_CHECK(hipEventRecord(c.kb_ev[4], sa));
       HIP_CHECK(hipStreamWaitEvent(s, c.kb_ev[4], 0));
     }
+    if (tm)  // the host's time to enqueue the loop (the device's is the tree_insert phase)
+      tm->host_ms("kb_loop_host", std::chrono::duration<double, std::milli>(
+                                      std::chrono::steady_clock::now() - host_t0).count());
   } else {
     for (size_t k = 0; k < nbk; ++k) {
       if (per_bucket) (void)hipMemsetAsync(ws, 0, 128, s);
@@ -1334,6 +1343,60 @@ int sheep_evaluate_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
   Ctx& c = ctx();
   require_aligned(d_uv, "d_uv");
   evaluate_dev(c, d_uv, m, d_parts, d_rank, n_ids, n_parts, out, pick(c, stream));
+  API_END
+}
+
+static void partition_edges_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                                const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts,
+                                uint32_t* d_out, uint64_t* part_start, hipStream_t s) {
+  require_records(m, "partition edges");
+  if (n_parts == 0 || n_parts > 32768) throw ApiError(-EINVAL, "n_parts must be in [1, 32768]");
+  const uint64_t mm = std::max<uint64_t>(m, 1);
+  uint64_t* items = (uint64_t*)c.scratch.get("e_items", mm * 8);
+  uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", mm * 8);
+  uint32_t* rtmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(mm) * 4);
+  unsigned long long* dstart = (unsigned long long*)c.scratch.get("pe_start", ((size_t)n_parts + 1) * 8);
+  launch_partition_edges(d_uv, m, d_parts, d_rank, n_ids, n_parts, items, items_b, rtmp, d_out,
+                         dstart, c.d_err, s);
+  HIP_CHECK(hipMemcpyAsync(part_start, dstart, ((size_t)n_parts + 1) * 8, hipMemcpyDeviceToHost, s));
+  check_err(c, s);  // synchronises; -ERANGE for an id outside the sequence or a vertex without part
+}
+
+int sheep_partition_edges_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
+                              const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts,
+                              uint32_t* d_out, uint64_t* part_start, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  require_aligned(d_uv, "d_uv");
+  partition_edges_dev(c, d_uv, m, d_parts, d_rank, n_ids, n_parts, d_out, part_start, pick(c, stream));
+  API_END
+}
+
+int sheep_partition_edges(const uint32_t* edges_uv, uint64_t m, const int16_t* parts,
+                          uint32_t n_parts_vid, const uint32_t* seq, uint32_t n_seq, uint32_t n_parts,
+                          uint32_t* out_uv, uint64_t* part_start) {
+  API_BEGIN
+  Ctx& c = ctx();
+  hipStream_t s = c.stream;
+  uint32_t n_ids = n_parts_vid;
+  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
+  for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
+  HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));
+  if (n_parts_vid)
+    HIP_CHECK(hipMemcpyAsync(dparts, parts, (size_t)n_parts_vid * 2, hipMemcpyHostToDevice, s));
+  uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)std::max<uint32_t>(n_seq, 1) * 4);
+  if (n_seq) HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
+  uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
+  launch_fill(rank, INV, n_ids, s);
+  launch_rank_scatter(dseq, n_seq, rank, c.d_err, s);
+  uint32_t* out = (uint32_t*)c.scratch.get("pe_out", std::max<uint64_t>(8 * m, 8));
+  partition_edges_dev(c, uv, m, dparts, rank, n_ids, n_parts, out, part_start, s);
+  const uint64_t kept = part_start[n_parts];
+  if (kept) HIP_CHECK(hipMemcpyAsync(out_uv, out, 8 * kept, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
   API_END
 }
 

@@ -195,4 +195,74 @@ void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const
   }
 }
 
+// ---- graph2tree -p K -o OUT: the records of each part (writePartitionedGraph, partition.cpp:
+// 588-630).  The reference walks the graph node by node (X ascending) and writes every edge
+// (X, Y) with X < Y to the part of its lower-sequence endpoint, so a part's file lists its
+// edges by X, each X's in adjacency order (record order for EdgeGraph); self-loops are skipped.
+// Here: key (X, record) sorted stably by X, re-keyed (part, record) and sorted stably by part:
+// the records come out grouped by part, each part in the writer's order.
+__global__ void k_pe_keys(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, uint64_t* items) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint2 e = uv[i];
+    const uint32_t x = e.x == e.y ? n_ids : min(e.x, e.y);  // n_ids: self-loops sort last
+    items[i] = ((uint64_t)x << 32) | (uint32_t)i;
+  }
+}
+
+__global__ void k_pe_part_keys(const uint64_t* __restrict__ sorted, uint64_t m,
+                               const uint2* __restrict__ uv, const int16_t* __restrict__ parts,
+                               const uint32_t* __restrict__ pos, uint32_t n_ids, uint32_t n_parts,
+                               uint64_t* items, uint32_t* err) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t it = sorted[j];
+    const uint32_t i = (uint32_t)it;
+    uint32_t p = n_parts;  // self-loops: after every part
+    if ((uint32_t)(it >> 32) != n_ids) {
+      const uint2 e = uv[i];
+      const uint32_t x = min(e.x, e.y), y = max(e.x, e.y);
+      if (y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
+      const int16_t q = pos[x] < pos[y] ? parts[x] : parts[y];
+      if (q < 0 || (uint32_t)q >= n_parts) atomicOr(err, ERR_RANGE);  // a vertex without a part
+      else p = (uint32_t)q;
+    }
+    items[j] = ((uint64_t)p << 32) | i;
+  }
+}
+
+// out: the (X, Y) pairs in order; pstart[q] (q <= n_parts) = first position of part q.
+__global__ void k_pe_emit(const uint64_t* __restrict__ sorted, uint64_t m, const uint2* __restrict__ uv,
+                          uint32_t n_parts, uint2* out, unsigned long long* pstart) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= m;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t prev = j ? (int64_t)(sorted[j - 1] >> 32) : -1;
+    const int64_t cur = j < m ? (int64_t)(sorted[j] >> 32) : (int64_t)n_parts + 1;
+    for (int64_t q = prev + 1; q <= cur && q <= (int64_t)n_parts; ++q) pstart[q] = j;
+    if (j < m && cur < (int64_t)n_parts) {
+      const uint2 e = uv[(uint32_t)sorted[j]];
+      out[j] = make_uint2(min(e.x, e.y), max(e.x, e.y));
+    }
+  }
+}
+
+void launch_partition_edges(const uint32_t* uv, uint64_t m, const int16_t* parts, const uint32_t* pos,
+                            uint32_t n_ids, uint32_t n_parts, uint64_t* items, uint64_t* items_b,
+                            uint32_t* rtmp, uint32_t* out, unsigned long long* pstart, uint32_t* err,
+                            hipStream_t s) {
+  int xb = 0, pb = 0;
+  for (uint32_t v = n_ids; v; v >>= 1) ++xb;    // keys <= n_ids
+  for (uint32_t v = n_parts; v; v >>= 1) ++pb;  // keys <= n_parts
+  hipLaunchKernelGGL(k_pe_keys, dim3(ev_grid(m)), dim3(EV_BLOCK), 0, s, (const uint2*)uv, m, n_ids,
+                     items);
+  const uint64_t* by_x = radix_sort_u64(items, items_b, items, m, 0, xb, rtmp, s);
+  uint64_t* other = by_x == items ? items_b : items;
+  hipLaunchKernelGGL(k_pe_part_keys, dim3(ev_grid(m)), dim3(EV_BLOCK), 0, s, by_x, m,
+                     (const uint2*)uv, parts, pos, n_ids, n_parts, other, err);
+  const uint64_t* by_part = radix_sort_u64(other, other == items ? items_b : items, other, m, 0, pb,
+                                           rtmp, s);
+  hipLaunchKernelGGL(k_pe_emit, dim3(ev_grid(m + 1)), dim3(EV_BLOCK), 0, s, by_part, m,
+                     (const uint2*)uv, n_parts, (uint2*)out, pstart);
+}
+
 }  // namespace sheep

@@ -193,6 +193,13 @@ void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const
                      const uint32_t* deg, uint32_t n_ids, uint32_t k, uint64_t* keys,
                      uint64_t* keys_b, uint32_t* rtmp, unsigned long long* ws, uint32_t* err,
                      hipStream_t s);
+// graph2tree -p K -o OUT (sheep_eval.hip): the non-self-loop records as (min, max) pairs,
+// grouped by the part of their lower-sequence endpoint, each part in (min, record) order.
+// items / items_b: m u64; rtmp: rsort_tmp_words(m); out: 2m u32; pstart: n_parts + 1 u64.
+void launch_partition_edges(const uint32_t* uv, uint64_t m, const int16_t* parts, const uint32_t* pos,
+                            uint32_t n_ids, uint32_t n_parts, uint64_t* items, uint64_t* items_b,
+                            uint32_t* rtmp, uint32_t* out, unsigned long long* pstart, uint32_t* err,
+                            hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

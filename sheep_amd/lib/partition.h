@@ -9,6 +9,11 @@
 // same libstdc++ std::sort is called here on the same ranges in the same order.
 #pragma once
 #include <algorithm>
+#include <atomic>
+#include <charconv>
+#include <cassert>
+#include <string>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -191,10 +196,56 @@ class Partition {
   }
 
   // writePartitionedGraph (partition.cpp:588-630): edge (X,Y), X<Y, goes to the part of the
-  // lower-sequence endpoint; one "%s%04d" file per part.
-  template <typename GraphType, typename WriterType = SNAPWriter>
-  void writePartitionedGraph(GraphType const& graph, std::vector<vid_t> const& seq,
+  // lower-sequence endpoint; one "%s%04d" file per part.  The records are grouped by part on
+  // the GPU (sheep_partition_edges: X ascending, then record order, as the node-by-node walk
+  // below writes them) and the part files are formatted and written by parallel host threads.
+  void writePartitionedGraph(EdgeGraph const& graph, std::vector<vid_t> const& seq,
                              char const* prefix) const {
+    part_t const max_part = *std::max_element(parts.cbegin(), parts.cend());
+    assert(max_part < 10000);
+    const uint32_t np = (uint32_t)max_part + 1;
+    std::vector<uint32_t> out(2 * std::max<size_t>(graph.records(), 1));
+    std::vector<uint64_t> start(np + 1);
+    sheep_check(sheep_partition_edges(graph.records_data(), graph.records(), parts.data(),
+                                      (uint32_t)parts.size(), seq.data(), (uint32_t)seq.size(), np,
+                                      out.data(), start.data()),
+                "writePartitionedGraph");
+    std::vector<char> name(strlen(prefix) + 16);
+    std::vector<std::string> names(np);
+    for (uint32_t p = 0; p < np; ++p) {
+      snprintf(name.data(), name.size(), "%s%04d", prefix, (int)p);
+      names[p] = name.data();
+    }
+    std::atomic<uint32_t> next(0);
+    std::atomic<bool> failed(false);
+    auto work = [&] {
+      std::vector<char> buf;
+      for (uint32_t p; (p = next++) < np;) {
+        const uint64_t b = start[p], e = start[p + 1];
+        buf.resize((e - b) * 22 + 1);
+        char* w = buf.data();
+        for (uint64_t i = b; i < e; ++i) {
+          w = std::to_chars(w, w + 11, out[2 * i]).ptr;
+          *w++ = ' ';
+          w = std::to_chars(w, w + 11, out[2 * i + 1]).ptr;
+          *w++ = '\n';
+        }
+        FILE* f = fopen(names[p].c_str(), "wb");
+        if (!f || fwrite(buf.data(), 1, w - buf.data(), f) != (size_t)(w - buf.data())) failed = true;
+        if (f) fclose(f);
+      }
+    };
+    const unsigned nt = std::max(1u, std::min<unsigned>(np, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    if (failed) throw std::runtime_error(std::string("cannot write the part files ") + prefix + "*");
+  }
+
+  // The node-by-node walk of the reference (any GraphType with the LLAMA iterators).
+  template <typename GraphType, typename WriterType = SNAPWriter>
+  void writePartitionedGraph_walk(GraphType const& graph, std::vector<vid_t> const& seq,
+                                  char const* prefix) const {
     std::vector<jnid_t> pos(*std::max_element(seq.cbegin(), seq.cend()) + 1, INVALID_JNID);
     for (jnid_t i = 0; i != seq.size(); ++i) pos[seq[i]] = i;
     auto w = open_writers<WriterType>(prefix);

@@ -445,3 +445,31 @@ def test_graph2tree_all_self_loops_many_ids(oracle, gpu):
     assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
     assert (p == 0xFFFFFFFF).all() and (w == 0).all()
+
+
+@pytest.mark.parametrize("scale,k", [(0, 4), (14, 16), (16, 300)])
+def test_partition_edges_writer_order(oracle, api, hep_edges, scale, k):
+    """sheep_partition_edges (graph2tree -p K -o OUT on the GPU) against the reference's
+    node-by-node writer restated in numpy: per part, the pairs (X < Y) in X order, then record
+    order; self-loops skipped; the lower-sequence endpoint's part (partition.cpp:588-630)."""
+    uv = hep_edges if scale == 0 else oracle.rmat(scale, 16, scale)
+    seq = oracle.degree_sequence(uv)
+    p, w = oracle.build_tree(uv, seq)
+    parts = oracle.PartTree(p, w).partition(seq, k)
+    got = api.partition_edges(uv, parts, seq)
+    pos = np.full(parts.size, -1, np.int64)
+    pos[seq] = np.arange(seq.size)
+    x = uv.min(axis=1).astype(np.int64)
+    y = uv.max(axis=1).astype(np.int64)
+    keep = x != y
+    idx = np.nonzero(keep)[0]
+    owner = np.where(pos[x[idx]] < pos[y[idx]], parts[x[idx]], parts[y[idx]])
+    order = np.lexsort((idx, x[idx], owner))  # by part, then X, then record
+    assert len(got) == int(parts.max()) + 1
+    at = 0
+    for q, g in enumerate(got):
+        sel = order[at:at + g.shape[0]]
+        assert (owner[sel] == q).all()
+        assert np.array_equal(g[:, 0], x[idx][sel]) and np.array_equal(g[:, 1], y[idx][sel])
+        at += g.shape[0]
+    assert at == idx.size
