@@ -47,6 +47,24 @@ extern "C" {
  * Replaces the process/device setup around MPI_Init in graph2tree.cpp:134-157. */
 int sheep_gpu_init(int device);
 
+/* ---- records resident in HBM (the graph LLAMA keeps in RAM, graph_wrapper.h:43-63) --------
+ * sheep_records_register: the host records [uv, uv + 2m) are immutable until
+ * sheep_records_release(uv); the library keeps ONE device copy, and every host-pointer call
+ * given exactly (uv, m) uses it instead of uploading the records again.
+ * sheep_records_load_dat: reads the XS1 records of a .dat file (all of them, or the contiguous
+ * range of part/num_parts, 1-based, as graph2tree -l; the weight dropped) through pinned
+ * staging buffers straight into a registered device copy, filling uv_out (cap records) on the
+ * host meanwhile; uv_out NULL: *m_out only (size query).  *max_id_out = max id + 1 of the
+ * range.  Release with sheep_records_release(uv_out). */
+int sheep_records_register(const uint32_t* uv, uint64_t m);
+int sheep_records_release(const uint32_t* uv);
+int sheep_records_load_dat(const char* path, uint64_t part, uint64_t num_parts, uint32_t* uv_out,
+                           uint64_t cap, uint64_t* m_out, uint32_t* max_id_out);
+/* The same ingest into caller device memory d_uv (cap records; NULL: size query only).
+ * Synchronises the stream. */
+int sheep_read_dat_dev(const char* path, uint64_t part, uint64_t num_parts, uint32_t* d_uv,
+                       uint64_t cap, uint64_t* m_out, uint32_t* max_id_out, void* stream);
+
 /* Free all device scratch held by the library on the current device. */
 int sheep_release(void);
 

@@ -99,6 +99,10 @@ def lib():
         "sheep_graph2tree_multi_local": [vp, vp, c.c_uint32, c.c_uint32, c.c_int, u32p, u32p, u32p,
                                          u32p],
         "sheep_set_option": [c.c_char_p, c.c_longlong],
+        "sheep_records_register": [u32p, c.c_uint64],
+        "sheep_records_release": [u32p],
+        "sheep_records_load_dat": [c.c_char_p, c.c_uint64, c.c_uint64, u32p, c.c_uint64, vp, vp],
+        "sheep_read_dat_dev": [c.c_char_p, c.c_uint64, c.c_uint64, u32p, c.c_uint64, vp, vp, vp],
         "sheep_get_option": [c.c_char_p, c.c_void_p],
         "sheep_partition": [u32p, u32p, c.c_uint32, u32p, vp, c.c_uint32, c.c_double, vp,
                             c.c_uint32, vp],

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <mutex>
 #include <thread>
@@ -261,6 +262,14 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
   int b = 0;
   while (v) { ++b; v >>= 1; }
   return b;
+}
+
+// The device copy of host records: a registered range's, else one upload into "h_uv".
+static uint32_t* upload_records(Ctx& c, const uint32_t* edges_uv, uint64_t m, hipStream_t s) {
+  for (const Ctx::Registered& r : c.registered)
+    if (r.host == edges_uv && r.m == m) return r.dev;
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
+  return uv;
 }
 
 // ---- device-level building blocks ---------------------------------------------------------
@@ -1362,6 +1371,146 @@ static void partition_edges_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const 
   check_err(c, s);  // synchronises; -ERANGE for an id outside the sequence or a vertex without part
 }
 
+// ---- records resident in HBM ---------------------------------------------------------------
+
+int sheep_records_register(const uint32_t* uv, uint64_t m) {
+  API_BEGIN
+  Ctx& c = ctx();
+  if (!uv) throw ApiError(-EINVAL, "null records");
+  for (const Ctx::Registered& r : c.registered)
+    if (r.host == uv) throw ApiError(-EBUSY, "records already registered");
+  uint32_t* dev = nullptr;
+  HIP_CHECK(hipMalloc(&dev, std::max<uint64_t>(8 * m, 8)));
+  if (m) HIP_CHECK(hipMemcpy(dev, uv, 8 * m, hipMemcpyHostToDevice));
+  c.registered.push_back({uv, m, dev});
+  API_END
+}
+
+int sheep_records_release(const uint32_t* uv) {
+  API_BEGIN
+  Ctx& c = ctx();
+  for (size_t i = 0; i < c.registered.size(); ++i)
+    if (c.registered[i].host == uv) {
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+      (void)hipFree(c.registered[i].dev);
+      c.registered.erase(c.registered.begin() + i);
+      return SHEEP_OK;
+    }
+  throw ApiError(-ENOENT, "records not registered");
+  API_END
+}
+
+// XS1 records of a .dat file: every complete record (LLAMA's load), or the contiguous range of
+// part/num_parts (1-based, graph2tree -l, graph_wrapper.h:48-49).  Returns the open file.
+static FILE* open_dat(const char* path, uint64_t part, uint64_t num_parts, uint64_t* lo,
+                      uint64_t* hi) {
+  if (!path) throw ApiError(-EINVAL, "null path");
+  FILE* f = fopen(path, "rb");
+  if (!f) throw ApiError(-ENOENT, std::string("cannot open ") + path);
+  if (fseeko(f, 0, SEEK_END) != 0) { fclose(f); throw ApiError(-EIO, "seek"); }
+  const uint64_t R = (uint64_t)ftello(f) / 12;
+  *lo = 0;
+  *hi = R;
+  if (num_parts) {
+    if (part < 1 || part > num_parts) { fclose(f); throw ApiError(-EINVAL, "part must be in [1, num_parts]"); }
+    *lo = R * (part - 1) / num_parts;
+    *hi = R * part / num_parts;
+  }
+  return f;
+}
+
+// Streams records [lo, lo + m) to dev (2m u32) through two pinned staging buffers: the file read
+// of chunk i+1 overlaps the upload and the weight-stripping kernel of chunk i; host (nullable)
+// receives the pairs too.  Returns max id + 1.  Synchronises s.
+static uint32_t ingest_dat(Ctx& c, FILE* f, uint64_t lo, uint64_t m, uint32_t* dev, uint32_t* host,
+                           hipStream_t s) {
+  constexpr uint64_t CH = 1ull << 22;  // records per chunk (48 MB)
+  uint32_t* pin[2] = {nullptr, nullptr};
+  uint32_t* raw[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  auto cleanup = [&] {
+    (void)hipStreamSynchronize(s);
+    for (int i = 0; i < 2; ++i) {
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      if (raw[i]) (void)hipFree(raw[i]);
+      if (done[i]) (void)hipEventDestroy(done[i]);
+    }
+  };
+  uint32_t mx = 0;
+  try {
+    for (int i = 0; i < 2; ++i) {
+      HIP_CHECK(hipHostMalloc((void**)&pin[i], CH * 12, hipHostMallocDefault));
+      HIP_CHECK(hipMalloc(&raw[i], CH * 12));
+      HIP_CHECK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+    }
+    uint32_t* dmax = (uint32_t*)c.scratch.get("ingest_max", 4);
+    HIP_CHECK(hipMemsetAsync(dmax, 0, 4, s));
+    if (fseeko(f, (off_t)(lo * 12), SEEK_SET) != 0) throw ApiError(-EIO, "seek");
+    for (uint64_t b = 0, k = 0; b < m; b += CH, ++k) {
+      const int i = (int)(k & 1);
+      const uint64_t n = std::min(CH, m - b);
+      if (k >= 2) HIP_CHECK(hipEventSynchronize(done[i]));  // chunk k-2's upload is done
+      if (fread(pin[i], 12, n, f) != n) throw ApiError(-EIO, "short read");
+      HIP_CHECK(hipMemcpyAsync(raw[i], pin[i], n * 12, hipMemcpyHostToDevice, s));
+      launch_strip_xs1(raw[i], n, dev + 2 * b, dmax, s);
+      HIP_CHECK(hipEventRecord(done[i], s));
+      if (host)
+        for (uint64_t j = 0; j < n; ++j) {
+          host[2 * (b + j)] = pin[i][3 * j];
+          host[2 * (b + j) + 1] = pin[i][3 * j + 1];
+        }
+    }
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned, dmax, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    mx = c.h_pinned[0];
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
+  return mx;
+}
+
+int sheep_records_load_dat(const char* path, uint64_t part, uint64_t num_parts, uint32_t* uv_out,
+                           uint64_t cap, uint64_t* m_out, uint32_t* max_id_out) {
+  API_BEGIN
+  Ctx& c = ctx();
+  uint64_t lo, hi;
+  std::unique_ptr<FILE, int (*)(FILE*)> f(open_dat(path, part, num_parts, &lo, &hi), fclose);
+  const uint64_t m = hi - lo;
+  if (m_out) *m_out = m;
+  if (!uv_out) return SHEEP_OK;  // size query
+  if (cap < m) throw ApiError(-ERANGE, "uv_out holds fewer records than the range");
+  for (const Ctx::Registered& r : c.registered)
+    if (r.host == uv_out) throw ApiError(-EBUSY, "records already registered");
+  uint32_t* dev = nullptr;
+  HIP_CHECK(hipMalloc(&dev, std::max<uint64_t>(8 * m, 8)));
+  try {
+    const uint32_t mx = ingest_dat(c, f.get(), lo, m, dev, uv_out, c.stream);
+    if (max_id_out) *max_id_out = mx;
+  } catch (...) {
+    (void)hipFree(dev);
+    throw;
+  }
+  c.registered.push_back({uv_out, m, dev});
+  API_END
+}
+
+int sheep_read_dat_dev(const char* path, uint64_t part, uint64_t num_parts, uint32_t* d_uv,
+                       uint64_t cap, uint64_t* m_out, uint32_t* max_id_out, void* stream) {
+  API_BEGIN
+  Ctx& c = ctx();
+  uint64_t lo, hi;
+  std::unique_ptr<FILE, int (*)(FILE*)> f(open_dat(path, part, num_parts, &lo, &hi), fclose);
+  const uint64_t m = hi - lo;
+  if (m_out) *m_out = m;
+  if (!d_uv) return SHEEP_OK;  // size query
+  if (cap < m) throw ApiError(-ERANGE, "d_uv holds fewer records than the range");
+  const uint32_t mx = ingest_dat(c, f.get(), lo, m, d_uv, nullptr, pick(c, stream));
+  if (max_id_out) *max_id_out = mx;
+  API_END
+}
+
 int sheep_partition_edges_dev(const uint32_t* d_uv, uint64_t m, const int16_t* d_parts,
                               const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts,
                               uint32_t* d_out, uint64_t* part_start, void* stream) {
@@ -1381,8 +1530,7 @@ int sheep_partition_edges(const uint32_t* edges_uv, uint64_t m, const int16_t* p
   uint32_t n_ids = n_parts_vid;
   for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
   for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
   HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));
   if (n_parts_vid)
@@ -1582,8 +1730,7 @@ int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int
   HIP_CHECK(hipMemcpyAsync(&hn, d_n, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   n_ids = (uint32_t)hn;
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   const size_t n = std::max<uint32_t>(n_ids, 1);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", n * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", n * 4);
@@ -1608,8 +1755,7 @@ int sheep_build_tree_multi(const uint32_t* edges_uv, uint64_t m, const uint32_t*
   if (n_seq == 0) return SHEEP_OK;
   // the index size of JTree (jtree.h:113): max(seq) + 1, the same on every rank
   const uint32_t n_rank = *std::max_element(seq, seq + n_seq) + 1;
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_seq * 4);
   HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
   uint32_t* parent = (uint32_t*)c.scratch.get("h_parent", (size_t)n_seq * 4);
@@ -1734,8 +1880,7 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
     throw ApiError(-EINVAL, "degree_mode");
   if (n_ids == 0)
     for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", 8 * m);
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
   uint32_t* seq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_ids * 4);
@@ -1758,8 +1903,7 @@ int sheep_evaluate(const uint32_t* edges_uv, uint64_t m, const int16_t* parts, u
   uint32_t n_ids = n_parts_vid;
   for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
   for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
   HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));  // INVALID_PART = -1
   if (n_parts_vid)
@@ -1781,8 +1925,7 @@ int sheep_build_tree(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq, 
   hipStream_t s = c.stream;
   if (n_seq == 0) return SHEEP_OK;
   uint32_t n_rank = *std::max_element(seq, seq + n_seq) + 1;  // reference index size, jtree.h:113
-  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", 8 * m);
-  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
+  uint32_t* uv = upload_records(c, edges_uv, m, s);
   uint32_t* dseq = (uint32_t*)c.scratch.get("h_seq", (size_t)n_seq * 4);
   HIP_CHECK(hipMemcpyAsync(dseq, seq, (size_t)n_seq * 4, hipMemcpyHostToDevice, s));
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_rank * 4);

@@ -70,6 +70,10 @@ struct Ctx {
   std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
   int ls_live = 0;                     // live lockstep sessions (sheep_ls_*) on this device
   struct Comm* comm = nullptr;         // this rank's communicator (sheep_comm_init), if any
+  // host record ranges declared immutable (sheep_records_register / sheep_records_load_dat)
+  // and their device copies: host-pointer calls on them upload nothing
+  struct Registered { const uint32_t* host; uint64_t m; uint32_t* dev; };
+  std::vector<Registered> registered;
 };
 
 Ctx& ctx();  // this thread's context for the current device (sheep_gpu_init)
@@ -200,6 +204,8 @@ void launch_partition_edges(const uint32_t* uv, uint64_t m, const int16_t* parts
                             uint32_t n_ids, uint32_t n_parts, uint64_t* items, uint64_t* items_b,
                             uint32_t* rtmp, uint32_t* out, unsigned long long* pstart, uint32_t* err,
                             hipStream_t s);
+// XS1 records {u32 tail, u32 head, f32 weight} -> (tail, head) pairs; max id + 1 into *max_id.
+void launch_strip_xs1(const uint32_t* raw, uint64_t n, uint32_t* uv, uint32_t* max_id, hipStream_t s);
 void launch_merge(uint32_t* parent_a, uint32_t* pst_a, const uint32_t* parent_b,
                   const uint32_t* pst_b, uint32_t n, uint32_t* jump, hipStream_t s);
 void launch_rmat(uint32_t* uv, int scale, uint64_t seed, uint64_t e_begin, uint64_t e_end,

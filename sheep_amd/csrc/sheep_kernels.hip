@@ -2509,6 +2509,24 @@ void launch_max_ptrs_i64(int64_t* dst, const int64_t* const* srcs, int P, size_t
   if (n) hipLaunchKernelGGL((k_reduce_ptrs<int64_t, true>), dim3(grid_for(n)), dim3(BLOCK), 0, s, dst, srcs, P, n);
 }
 
+// ---- .dat ingest (LLAMA's load_direct of XS1 records, graph_wrapper.h:43-63) -----------------
+__global__ void k_strip_xs1(const uint32_t* __restrict__ raw, uint64_t n, uint32_t* __restrict__ uv,
+                            uint32_t* max_id) {
+  uint32_t mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t t = raw[3 * i], h = raw[3 * i + 1];
+    ((uint2*)uv)[i] = make_uint2(t, h);
+    mx = max(mx, max(t, h) + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(max_id, mx);
+}
+
+void launch_strip_xs1(const uint32_t* raw, uint64_t n, uint32_t* uv, uint32_t* max_id, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_strip_xs1, dim3(grid_for(n)), dim3(BLOCK), 0, s, raw, n, uv, max_id);
+}
+
 __global__ void k_iota(uint32_t* p, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = i;
 }

@@ -237,3 +237,16 @@ def graph2tree_multi_local(shards, n_ids, mode=capi.DEGREE_LLAMA):
               ctypes.cast(ms, ctypes.c_void_p), P, n_ids, mode, _p(out[0]), _p(out[1]), _p(out[2]),
               ctypes.byref(n_seq))
     return out[0], out[1], out[2], n_seq.value
+
+
+def read_dat(path, part=0, num_parts=0, device="cuda"):
+    """XS1 records of a .dat file (or the part/num_parts range, 1-based as graph2tree -l)
+    straight into HBM through pinned staging: (uv (m, 2) uint32 tensor, max id + 1)."""
+    m = ctypes.c_uint64(0)
+    capi.call("sheep_read_dat_dev", str(path).encode(), part, num_parts, None, 0, ctypes.byref(m),
+              None, _stream())
+    uv = torch.empty((max(m.value, 1), 2), dtype=torch.uint32, device=device)
+    mx = ctypes.c_uint32(0)
+    capi.call("sheep_read_dat_dev", str(path).encode(), part, num_parts, _p(uv), m.value,
+              ctypes.byref(m), ctypes.byref(mx), _stream())
+    return uv[:m.value], mx.value

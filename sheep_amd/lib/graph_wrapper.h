@@ -17,10 +17,12 @@
 
 #include "defs.h"
 #include "readerwriter.h"
+#include "sheep_call.h"
 
 class EdgeGraph {
   std::vector<uint32_t> uv_;  // 2 * m
-  vid_t max_vid_ = 0;         // max id + 1 over the whole file
+  vid_t max_vid_ = 0;         // max id + 1 over the whole file (over the part, loaded to_device)
+  mutable const uint32_t* reg_ = nullptr;  // uv_ registered with the library (one device copy)
   mutable std::vector<uint64_t> off_;
   mutable std::vector<uint32_t> adj_;
   mutable size_t num_nodes_ = 0;
@@ -47,6 +49,51 @@ class EdgeGraph {
 
  public:
   EdgeGraph() = default;
+  EdgeGraph(EdgeGraph const&) = delete;
+  EdgeGraph& operator=(EdgeGraph const&) = delete;
+  EdgeGraph(EdgeGraph&& o) noexcept { *this = std::move(o); }
+  ~EdgeGraph() {
+    if (reg_) (void)sheep_records_release(reg_);
+  }
+
+  // to_device: a .dat file goes straight to HBM through pinned staging (sheep_records_load_dat)
+  // and stays there for every GPU call on this graph; the host copy is filled on the way.
+  EdgeGraph(char const* filename, size_t part, size_t num_parts, bool to_device) {
+    if (!to_device || !is_dat(filename)) {
+      *this = EdgeGraph(filename, part, num_parts);
+      if (to_device) this->to_device();
+      return;
+    }
+    uint64_t m = 0;
+    uint32_t mx = 0;
+    sheep_check(sheep_records_load_dat(filename, part, num_parts, nullptr, 0, &m, nullptr), "load");
+    uv_.resize(2 * std::max<uint64_t>(m, 1));
+    sheep_check(sheep_records_load_dat(filename, part, num_parts, uv_.data(), m, &m, &mx), "load");
+    uv_.resize(2 * m);
+    reg_ = uv_.data();
+    max_vid_ = mx;
+  }
+  EdgeGraph& operator=(EdgeGraph&& o) noexcept {
+    if (this != &o) {
+      if (reg_) (void)sheep_records_release(reg_);
+      uv_ = std::move(o.uv_);
+      max_vid_ = o.max_vid_;
+      off_ = std::move(o.off_);
+      adj_ = std::move(o.adj_);
+      num_nodes_ = o.num_nodes_;
+      reg_ = o.reg_;
+      o.reg_ = nullptr;
+    }
+    return *this;
+  }
+
+  // Keep one device copy of the records for the GPU calls that follow (idempotent).
+  void to_device() const {
+    if (reg_ || uv_.empty()) return;
+    sheep_check(sheep_records_register(uv_.data(), records()), "records");
+    reg_ = uv_.data();
+  }
+
   EdgeGraph(char const* filename, size_t part = 0, size_t num_parts = 0) {
     std::vector<uint32_t> all;
     if (is_dat(filename)) {

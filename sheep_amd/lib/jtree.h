@@ -49,6 +49,7 @@ class JTree {
     if (!opts.isSupported())
       throw std::invalid_argument("JTree: chordal-extension options are not built on MI355X");
     make_index(seq);
+    graph.to_device();
     std::vector<jnid_t> parent(seq.size());
     std::vector<esize_t> pst(seq.size());
     if (!seq.empty())
@@ -111,6 +112,7 @@ class JTree {
     if (!opts.isSupported())
       throw std::invalid_argument("JTree: chordal-extension options are not built on MI355X");
     make_index(seq);
+    graph.to_device();
     std::vector<jnid_t> parent(seq.size());
     std::vector<esize_t> pst(seq.size());
     if (!seq.empty())

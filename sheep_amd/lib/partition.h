@@ -178,6 +178,7 @@ class Partition {
   template <typename GraphType>
   void evaluate_gpu(GraphType const& graph, std::vector<vid_t> const& seq) const {
     uint64_t o[11];
+    graph.to_device();
     part_t max_part = *std::max_element(parts.cbegin(), parts.cend());
     sheep_check(sheep_evaluate(graph.records_data(), graph.records(), parts.data(),
                                (uint32_t)parts.size(), seq.data(), (uint32_t)seq.size(),
@@ -204,6 +205,7 @@ class Partition {
     part_t const max_part = *std::max_element(parts.cbegin(), parts.cend());
     assert(max_part < 10000);
     const uint32_t np = (uint32_t)max_part + 1;
+    graph.to_device();
     std::vector<uint32_t> out(2 * std::max<size_t>(graph.records(), 1));
     std::vector<uint64_t> start(np + 1);
     sheep_check(sheep_partition_edges(graph.records_data(), graph.records(), parts.data(),

@@ -29,6 +29,7 @@ inline std::vector<vid_t> edgeSequence(const uint32_t* uv, size_t m, vid_t n_ids
 // degreeSequence (sequence.h:52-63): LLAMA degrees (a self-loop counts once).
 template <typename GraphType>
 std::vector<vid_t> degreeSequence(GraphType const& graph) {
+  graph.to_device();
   return edgeSequence(graph.records_data(), graph.records(), graph.getMaxVid(), SHEEP_DEGREE_LLAMA);
 }
 
@@ -37,6 +38,7 @@ std::vector<vid_t> degreeSequence(GraphType const& graph) {
 // every rank gets the same sequence.
 template <typename GraphType>
 std::vector<vid_t> mpiSequence(GraphType const& graph) {
+  graph.to_device();
   std::vector<vid_t> seq(std::max<vid_t>(graph.getMaxVid(), 1));
   uint32_t n_seq = 0;
   sheep_check(sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),

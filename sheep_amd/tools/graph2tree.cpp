@@ -99,7 +99,7 @@ int main(int argc, char* argv[]) {
                          (!(use_mpi_sort || use_mpi_reduce) && strcmp(sequence_filename, "") == 0);
   try {
     if (jopts.verbose) printf("Loading %s...\n", graph_filename);
-    GraphWrapper graph(graph_filename, part, num_parts);
+    GraphWrapper graph(graph_filename, part, num_parts, true);  // records straight to HBM
     if (jopts.verbose) printf("Nodes:%zu Edges:%zu\n", graph.getNodes(), graph.getEdges());
     auto t_load = clk::now();
     if (is_leader) printf("Loaded graph in: %f seconds\n", secs(t_load - t0));

@@ -473,3 +473,38 @@ def test_partition_edges_writer_order(oracle, api, hep_edges, scale, k):
         assert np.array_equal(g[:, 0], x[idx][sel]) and np.array_equal(g[:, 1], y[idx][sel])
         at += g.shape[0]
     assert at == idx.size
+
+
+def test_dat_ingest_and_registered_records(oracle, api, tmp_path):
+    """sheep_read_dat_dev / sheep_records_load_dat (pinned staging -> HBM, the f32 weight
+    dropped) give the file's records for the whole file and every -l part, across the ingest's
+    4M-record chunks; registered records give the same results as uploaded ones."""
+    import ctypes
+
+    import torch
+    from sheep_amd import capi, device
+
+    uv = oracle.rmat(18, 16, 5)  # 4.2 M records: two ingest chunks
+    path = str(tmp_path / "r18.dat")
+    api.write_dat(path, uv)
+    got, mx = device.read_dat(path)
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), uv) and mx == int(uv.max()) + 1
+    m = uv.shape[0]
+    for part in (1, 2, 3):
+        lo, hi = m * (part - 1) // 3, m * part // 3
+        g, _ = device.read_dat(path, part, 3)
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), uv[lo:hi])
+    host = np.zeros((m, 2), np.uint32)
+    n = ctypes.c_uint64(0)
+    capi.call("sheep_records_load_dat", path.encode(), 0, 0, ctypes.c_void_p(host.ctypes.data), m,
+              ctypes.byref(n), None)
+    try:
+        assert np.array_equal(host, uv)
+        seq = api.degree_sequence(host)  # through the registered device copy
+        assert np.array_equal(seq, oracle.degree_sequence(uv))
+        t = api.build_tree(host, seq)
+        p, w = oracle.build_tree(uv, seq)
+        assert np.array_equal(t.parent, p) and np.array_equal(t.pst, w)
+    finally:
+        capi.call("sheep_records_release", ctypes.c_void_p(host.ctypes.data))
+    torch.cuda.synchronize()
