@@ -268,7 +268,8 @@ static inline int bits_for(uint64_t v) {  // number of significant bits
 static uint32_t* upload_records(Ctx& c, const uint32_t* edges_uv, uint64_t m, hipStream_t s) {
   for (const Ctx::Registered& r : c.registered)
     if (r.host == edges_uv && r.m == m) return r.dev;
-  uint32_t* uv = upload_records(c, edges_uv, m, s);
+  uint32_t* uv = (uint32_t*)c.scratch.get("h_uv", std::max<uint64_t>(8 * m, 8));
+  if (m) HIP_CHECK(hipMemcpyAsync(uv, edges_uv, 8 * m, hipMemcpyHostToDevice, s));
   return uv;
 }
 
