@@ -1,4 +1,4 @@
-"""Build a lab copy of libsheep_amd.so with one k_kb_map ablation (results WRONG, timing only):
+"""Build a lab copy of libsheep_amd.so with one kernel variant (ablations: results WRONG, timing only):
     python scripts/lab/build_ablation.py NAME  -> scripts/lab/libsheep_NAME.so
 Ablations patch the kernel text of a temporary copy; the product source is not touched."""
 import os
@@ -55,23 +55,86 @@ PATCHES = {
     "nokept": [("      if (it[r] != ~0ull) kept[pos + __popcll(bal & lt)] = it[r];", "      if (it[r] == 1ull) kept[0] = it[r];")],
     # no finds: every miss is taken as giant
     "nofind": [("    for (uint32_t act = miss; act;) {", "    for (uint32_t act = 0; act;) {")],
+    # partition tiles: 8K records (2 blocks / CU) or 4K (4 blocks / CU)
+    "pt512": [("static constexpr int PT_THREADS = 1024;", "static constexpr int PT_THREADS = 512;")],
+    "pt1k8": [("static constexpr int PT_ITEMS = 16;", "static constexpr int PT_ITEMS = 8;")],
+    "pt256": [("static constexpr int PT_THREADS = 1024;", "static constexpr int PT_THREADS = 256;")],
+    # degree scatter chunks of 16K records (64 KB LDS: 2 blocks / CU)
+    "dg16": [("static constexpr int DEGB_CHUNK = 32768;", "static constexpr int DEGB_CHUNK = 16384;")],
+    # partition cursors one per 128-B line (same-line atomics from every tile)
+    "ptpad": [("gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;",
+               "gbase[t] = c ? atomicAdd(&cursor[16 * t], (unsigned long long)c) : 0ull;"),
+              ("  cursor[t] = s[t];\n  hist[t] = 0;", "  cursor[16 * t] = s[t];\n  hist[t] = 0;")],
+    # partition without the LDS stage: each record is stored straight from registers to its
+    # reserved run (order inside a run by LDS-atomic order); 3 KB of LDS -> 2 blocks / CU
+    "ptdirect": [("  __shared__ uint64_t stage[PT_TILE];\n  __shared__ uint32_t hist[256], tstart[256]", "  __shared__ uint32_t hist[256], tstart[256]"),
+                 ("""      stage[tstart[part_digit(key, sh)] + li[k]] = rec[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < tile_n; j += PT_THREADS) {
+    uint64_t r = stage[j];
+    uint32_t d = part_digit(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
+    out[gbase[d] + (j - tstart[d])] = r;
+  }""", """      out[gbase[part_digit(key, sh)] + li[k]] = rec[k];
+    }
+  }""")],
+    # partition loads of 16 B per lane (two records; lab only: assumes 16-B aligned input)
+    "pt16b": [("""#pragma unroll
+  for (int k = 0; k < PT_ITEMS; ++k) {
+    uint32_t j = (uint32_t)k * PT_THREADS + t;
+    rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+  }""", """#pragma unroll
+  for (int k = 0; k < PT_ITEMS; k += 2) {
+    uint32_t j = (uint32_t)(k >> 1) * 2 * PT_THREADS + 2 * t;
+    if (j + 1 < tile_n) {
+      ulonglong2 q = *(const ulonglong2*)(in + tbase + j);
+      rec[k] = q.x; rec[k + 1] = q.y;
+    } else {
+      rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+      rec[k + 1] = 0ull;
+    }
+  }"""),
+              ("""    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      li[k]""", """    if ((uint32_t)(k >> 1) * 2 * PT_THREADS + 2 * t + (k & 1) < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      li[k]"""),
+              ("""    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      stage""", """    if ((uint32_t)(k >> 1) * 2 * PT_THREADS + 2 * t + (k & 1) < tile_n) {
+      uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
+      stage""")],
+    # fewer map blocks: the concurrent apply (the critical path) gets more of the chip
+    "mg256": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 256);")],
+    "mg192": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 192);")],
+    "mg320": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 320);")],
+    "mg384": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 384);")],
+    "mg128": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 128);")],
+}
+CAPI_PATCHES = {
+    "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],
 }
 
 
 def main():
     name = sys.argv[1]
     text = open(os.path.join(SRC, "sheep_kernels.hip")).read()
-    for a, b in PATCHES[name]:
-        assert a in text, a
-        text = text.replace(a, b)
+    for part in name.split("+"):
+        for a, b in PATCHES[part]:
+            assert a in text, a
+            text = text.replace(a, b)
     capi = open(os.path.join(SRC, "sheep_capi.cpp")).read()
     if name == "stamp":
         a = 'h[0], h[5], h[7], h[8], h[9], h[10], h[11], h[12]);'
         assert a in capi
         capi = capi.replace(a, a + '\n    fprintf(stderr, "map_phases_cycles load+bits %llu finds %llu label %llu lds %llu barA %llu flush %llu compact+barB+write %llu\\n", h[1], h[2], h[3], h[4], h[13], h[14], h[15]);')
+    for a, b in CAPI_PATCHES.get(name, []):
+        assert a in capi, a
+        capi = capi.replace(a, b)
     tmp = "/tmp/sheep_lab_%s" % name
     os.makedirs(tmp, exist_ok=True)
-    for f in ("powerlaw.h", "rmat.h", "sheep_internal.h"):
+    for f in ("powerlaw.h", "rmat.h", "sheep_internal.h", "sheep_comm.h"):
         open(os.path.join(tmp, f), "w").write(open(os.path.join(SRC, f)).read())
     open(os.path.join(tmp, "sheep_kernels.hip"), "w").write(text)
     open(os.path.join(tmp, "sheep_capi.cpp"), "w").write(capi.replace('"../../include/sheep_amd.h"', '"%s"' % os.path.join(ROOT, "include", "sheep_amd.h")))
@@ -80,7 +143,7 @@ def main():
            "-Wno-unused-result", "-shared", "-o", out, "-I", SRC, "-x", "hip",
            os.path.join(tmp, "sheep_kernels.hip"), "-x", "hip", os.path.join(SRC, "sheep_eval.hip"),
            "-x", "hip", os.path.join(tmp, "sheep_capi.cpp"), "-x", "hip",
-           os.path.join(SRC, "sheep_host.cpp")]
+           os.path.join(SRC, "sheep_host.cpp"), "-x", "hip", os.path.join(SRC, "sheep_comm.cpp"), "-ldl"]
     subprocess.run(cmd, check=True)
     print(out)
 

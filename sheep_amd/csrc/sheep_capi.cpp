@@ -663,16 +663,16 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     HIP_CHECK(hipMemcpyAsync(db, bounds.data(), nbins * 4, hipMemcpyHostToDevice, s));
     dbins = db;
     uint16_t* digits = (uint16_t*)c.scratch.get("item_bins", m * 2);
-    launch_edge_pass_bins(src, m, d_rank, n_rank, items, c.d_err, db, nbins, tmp, digits, s, part);
-    if (tm) tm->mark("edge_pass");
     unsigned long long* dstart = (unsigned long long*)c.scratch.get("bin_start", 513 * 8);
     // the bin starts reach the host before the scatter runs: the buckets are cut meanwhile
-    bin_sort_u64(items, items_b, m, db, nbins, tmp, dstart, digits, s, c.h_bstart, c.bins_ev);
+    uint64_t* out = group_by_bins(src, part, m, d_rank, n_rank, c.d_err, db, nbins, items, items_b,
+                                  tmp, digits, dstart, s, c.h_bstart, c.bins_ev);
+    if (tm) tm->mark("edge_pass");
     HIP_CHECK(hipEventSynchronize(c.bins_ev));
     std::vector<unsigned long long> hs(c.h_bstart, c.h_bstart + nbins + 1);
     given = buckets_from_bins(bounds, hs, m, n_seq);
-    sorted = items_b;
-    spare = items;
+    sorted = out;
+    spare = out == items ? items_b : items;
   } else {
     launch_edge_pass_tiles(src, m, d_rank, n_rank, pst_count ? nullptr : d_pst, items, c.d_err,
                            lo_bit, rsort_first_width(top + 1 - lo_bit), tmp, s, part);
@@ -851,17 +851,16 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
     src = (const uint32_t*)items_b;
   }
-  launch_edge_pass_bins(src, m, d_rank, n_rank, items, d_err, L.bins, nb, tmp, digits, s, part);
   unsigned long long* dstart = (unsigned long long*)sc.get("ls_bin_start", 513 * 8);
+  L.sorted = group_by_bins(src, part, m, d_rank, n_rank, d_err, L.bins, nb, items, items_b, tmp,
+                           digits, dstart, s);
   if (m) {
-    bin_sort_u64(items, items_b, m, L.bins, nb, tmp, dstart, digits, s);
     L.local_start.resize(nb + 1);
     HIP_CHECK(hipMemcpyAsync(L.local_start.data(), dstart, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
   } else {
     L.local_start.assign(nb + 1, 0ull);
   }
-  L.sorted = items_b;
   for (uint32_t i = 0; i < nb; ++i) counts_out[i] = L.local_start[i + 1] - L.local_start[i];
   *nb_out = nb;
 }

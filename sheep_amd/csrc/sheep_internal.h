@@ -139,6 +139,15 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
                   hipStream_t s,
                   unsigned long long* h_start = nullptr /* pinned: bin_start, before the scatter */,
                   hipEvent_t started = nullptr /* recorded once h_start is written */);
+// Records (uv, or k_part's pre records) -> items (hi << 32 | lo) grouped by hi bin: the edge
+// pass (items, each item's bin into digits (m u16), tile bin counts), then the scatter.
+// Returns the buffer holding the result (items_b; items is then free); uv may be items_b.
+// bin_start, h_start, started: as bin_sort_u64.
+uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
+                        uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                        uint64_t* items, uint64_t* items_b, uint32_t* tmp, uint16_t* digits,
+                        unsigned long long* bin_start, hipStream_t s,
+                        unsigned long long* h_start = nullptr, hipEvent_t started = nullptr);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,

@@ -30,6 +30,20 @@ static constexpr int ITEMS = 16;
 static constexpr int TILE = BLOCK * ITEMS;  // keys per radix/scan tile
 static constexpr int MAX_GRID = 256 * 8;    // 8 blocks of 256 per CU over 256 CUs
 
+// Compute units of the current device.
+static unsigned device_cus() {
+  static thread_local int cached_dev = -1;
+  static thread_local unsigned cached = 0;
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != cached_dev) {
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cached = n > 0 ? (unsigned)n : 256u;
+    cached_dev = dev;
+  }
+  return cached;
+}
+
 static inline unsigned grid_for(uint64_t n, int per_block = BLOCK) {
   uint64_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -1358,6 +1372,16 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
                      (uint16_t*)nullptr, 0);
 }
 
+uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
+                        uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                        uint64_t* items, uint64_t* items_b, uint32_t* tmp, uint16_t* digits,
+                        unsigned long long* bin_start, hipStream_t s,
+                        unsigned long long* h_start, hipEvent_t started) {
+  launch_edge_pass_bins(uv, m, rank, n_rank, items, err, bins, nb, tmp, digits, s, pre);
+  bin_sort_u64(items, items_b, m, bins, nb, tmp, bin_start, digits, s, h_start, started);
+  return items_b;
+}
+
 // ---------------------------------------------------------------------------------------
 // Partitioned rank gathers.  rank[] (4 B per id, 268 MB at RMAT-26) is far beyond L2 and the
 // stream evicts it from the Infinity Cache: gathered in stream order, every lookup is a 64-B
@@ -2353,7 +2377,10 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    const uint32_t* gx, bool defer, hipStream_t s) {
   if (e_end <= e_begin) return;
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
-  unsigned grid = (unsigned)std::min<uint64_t>(chunks, 512);  // 2 blocks per CU fit the LDS window
+  // One block per CU: the apply of the previous bucket (the loop's critical path) runs beside
+  // this map, and more map blocks slow it down more than they speed the map up (RMAT-26 tree
+  // phase 28.6 / 27.6 / 31.0 / 29.8 ms at 512 / 256 / 320 / 384 blocks; 192: 29.7).
+  unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
                      uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
@@ -2397,7 +2424,9 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   if (fold)
     hipLaunchKernelGGL(k_kb_fold, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                        0, s, (const uint32_t*)bitmap, B0, B1, uf, anchor, gbits, gx);
-  unsigned ug = grid_for((uint64_t)(B1 - B0) + 4096);
+  // the linked pre-bucket roots (device count) can outnumber the bucket's ranks many times
+  // over (hub buckets: ~500 ranks, ~0.3 M linked roots): a full grid, whatever the width
+  unsigned ug = MAX_GRID;
   auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
   hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,

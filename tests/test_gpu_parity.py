@@ -87,6 +87,7 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     (16, 24, 0, {"edge_part": 0}),  # direct gathers, hi bins
     (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
+    (18, 29, 0, {"bin_scatter": 0}),  # stable bin scatter
 ])
 def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
