@@ -111,6 +111,14 @@ PATCHES = {
     "mg320": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 320);")],
     "mg384": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 384);")],
     "mg128": [("std::min<uint64_t>(chunks, 512);", "std::min<uint64_t>(chunks, 128);")],
+    # bin scatter tiles of 8192 items, 512 threads, 64 KB stage: two blocks per CU
+    "bs512": [("static constexpr int BS_TILE = 2 * RS_TILE;", "static constexpr int BS_TILE = RS_TILE;"),
+              ("__global__ void __launch_bounds__(1024)\nk_bin_scatter(", "__global__ void __launch_bounds__(512)\nk_bin_scatter("),
+              ("  constexpr int NT = 1024, IT = BS_TILE / NT;\n  __shared__ uint64_t stage[BS_TILE];\n  __shared__ uint32_t hist[512], tstart[512], goff[512], wsum[NT / 64];",
+               "  constexpr int NT = 512, IT = BS_TILE / NT;\n  __shared__ uint64_t stage[BS_TILE];\n  __shared__ uint32_t hist[512], tstart[512], goff[512], wsum[NT / 64];"),
+              ("    goff[t] = offsets[(uint64_t)(2 * blockIdx.x) * 512 + t];\n  }\n  uint64_t it[IT];",
+               "    goff[t] = offsets[(uint64_t)blockIdx.x * 512 + t];\n  }\n  uint64_t it[IT];"),
+              ("dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,", "dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(512), 0, s,")],
 }
 CAPI_PATCHES = {
     "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],

@@ -1396,7 +1396,11 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // ---------------------------------------------------------------------------------------
 static constexpr int PT_THREADS = 1024;
 static constexpr int PT_ITEMS = 16;
-static constexpr int PT_TILE = PT_THREADS * PT_ITEMS;  // 16384 records, 128 KB LDS stage
+// k_part<MODE, NT> tiles are NT * PT_ITEMS records (8 B each staged in LDS): the first pass
+// uses 1024 threads (16384 records, 128 KB: one block per CU, which leaves room beside it for
+// the degree kernels it overlaps); the second runs alone and uses 512 (8192 records, 64 KB:
+// two blocks per CU, so one streams while the other is between barriers; RMAT-26 7.7 -> 6.3 ms).
+static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;
 
 
 // Global histogram of the y digits (the first partition's run sizes).
@@ -1428,23 +1432,24 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
   hist[t] = 0;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(PT_THREADS)
+template <int MODE, int NT>
+__global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh,
        const uint32_t* __restrict__ rank, uint32_t n_rank) {
-  __shared__ uint64_t stage[PT_TILE];
-  __shared__ uint32_t hist[256], tstart[256], hx[256], wsum[PT_THREADS / 64];
+  constexpr int TILE = NT * PT_ITEMS;
+  __shared__ uint64_t stage[TILE];
+  __shared__ uint32_t hist[256], tstart[256], hx[256], wsum[NT / 64];
   __shared__ unsigned long long gbase[256];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint64_t tbase = (uint64_t)blockIdx.x * PT_TILE;
-  const uint32_t tile_n = (uint32_t)min((uint64_t)PT_TILE, m - tbase);
+  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
   if (t < 256) { hist[t] = 0; hx[t] = 0; }
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
-    uint32_t j = (uint32_t)k * PT_THREADS + t;
+    uint32_t j = (uint32_t)k * NT + t;
     rec[k] = j < tile_n ? in[tbase + j] : 0ull;
   }
   if (MODE == 1) {  // (x, y) -> (x, ry)
@@ -1464,7 +1469,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
-    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+    if ((uint32_t)k * NT + t < tile_n) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
       li[k] = atomicAdd(&hist[part_digit(key, sh)], 1u);
       if (MODE == 0) atomicAdd(&hx[part_digit((uint32_t)rec[k], sh)], 1u);
@@ -1488,13 +1493,13 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
-    if ((uint32_t)k * PT_THREADS + t < tile_n) {
+    if ((uint32_t)k * NT + t < tile_n) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
       stage[tstart[part_digit(key, sh)] + li[k]] = rec[k];
     }
   }
   __syncthreads();
-  for (uint32_t j = t; j < tile_n; j += PT_THREADS) {
+  for (uint32_t j = t; j < tile_n; j += NT) {
     uint64_t r = stage[j];
     uint32_t d = part_digit(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
     out[gbase[d] + (j - tstart[d])] = r;
@@ -1522,8 +1527,8 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
     hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
   }
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
-  uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
-  hipLaunchKernelGGL(k_part<0>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, (const uint64_t*)uv, m,
+  uint64_t nt = (m + PT0_THREADS * PT_ITEMS - 1) / (PT0_THREADS * PT_ITEMS);
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS>), dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m,
                      mid, cursor, xhist, sh, (const uint32_t*)nullptr, n_rank);
 }
 
@@ -1533,9 +1538,9 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   const int sh = part_shift(n_rank);
   uint32_t* xhist = ws + 256;
   unsigned long long* cursor = (unsigned long long*)(ws + 512);
-  uint64_t nt = (m + PT_TILE - 1) / PT_TILE;
+  uint64_t nt = (m + PT1_THREADS * PT_ITEMS - 1) / (PT1_THREADS * PT_ITEMS);
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, xhist, cursor);
-  hipLaunchKernelGGL(k_part<1>, dim3((unsigned)nt), dim3(PT_THREADS), 0, s, mid, m,
+  hipLaunchKernelGGL((k_part<1, PT1_THREADS>), dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, m,
                      pre, cursor, xhist, sh, rank, n_rank);
 }
 
