@@ -9,7 +9,7 @@ import collections
 import re
 import sqlite3
 
-APPLY = ["k_kb_refresh", "k_kb_spine", "k_kb_zip", "k_kb_fold", "k_kb_union", "k_kb_label"]
+APPLY = ["k_kb_refresh", "k_kb_spine", "k_kb_zip", "k_kb_union", "k_kb_label"]
 OTHER = ["k_kb_map", "k_gb_rebase"]
 
 

@@ -119,6 +119,13 @@ PATCHES = {
               ("    goff[t] = offsets[(uint64_t)(2 * blockIdx.x) * 512 + t];\n  }\n  uint64_t it[IT];",
                "    goff[t] = offsets[(uint64_t)blockIdx.x * 512 + t];\n  }\n  uint64_t it[IT];"),
               ("dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,", "dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(512), 0, s,")],
+    # zipper without the jump hints (results unchanged: hints only)
+    "zipnojump": [("    tree_queue_body<0, 1, STATS, true, true>(src, src.np + nk,", "    tree_queue_body<0, 0, STATS, true, true>(src, src.np + nk,"),
+                  ("    tree_queue_body<0, 1, STATS, true, false>(src, nk,", "    tree_queue_body<0, 0, STATS, true, false>(src, nk,")],
+    # zipper parent loads as plain loads (L1/L2 cached) instead of agent-scope atomic loads
+    "zipplain": [("  if (LOAD == 0) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);", "  if (LOAD == 0) return *(volatile uint32_t*)p;")],
+    # zipper: no jump-hint load on the first step of a pending edge (most edges take one step)
+    "zipj2": [("    if (JUMP) {\n      const uint32_t j = jump[s.x];", "    if (JUMP && !(s.x == s.a && s.prev == INV)) {\n      const uint32_t j = jump[s.x];")],
 }
 CAPI_PATCHES = {
     "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],

@@ -1891,7 +1891,7 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, u
 // whose bit is not set yet) run the find, and those finds are batched: every lane first loads
 // its KM_R records and their bitmap words, then walks all of its misses' chains together (the
 // loads of different records interleave), and a miss that reaches the giant sets its bit for
-// the records that follow.  Bits are set by this map, by k_kb_fold (the bucket's marked ranks)
+// the records that follow.  Bits are set by this map, by k_kb_spine (the bucket's marked ranks)
 // and by k_kb_label (the bucket's ranks that ended in X's component); they are only ever
 // cleared by k_gb_rebase when X moves to another component (before the giant has formed).
 // A block takes chunks of KM_CHUNK records; marks and counts of ranks within KM_WIN of the
@@ -2131,20 +2131,36 @@ __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf
 // the zipper inserts (walking G's chain).  One thread per bitmap word; the forward search of
 // a word's last mark and the backward search of a word's first mark are symmetric, so every
 // mark gets exactly one incoming connection.
+// The same pass is the giant fold: every marked rank of the bucket ends in the anchor's
+// component (the spine joins all of them to G), and its union-find slot is still its own
+// (iota: nothing links an in-bucket rank before its bucket's union), so it is stored under
+// that component's root R directly — no find, no CAS (nothing before the bucket's union
+// reads in-bucket union-find slots).  k_kb_union then skips the links between two marked
+// ranks (already in one tree).  gbits (nullable): the marked ranks are giant members; when
+// the bitmap's reference vertex *gx lies in the anchor's component they are set there too
+// (see k_kb_map).
 __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
-                           uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit) {
+                           uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit,
+                           uint32_t* uf, uint32_t anchor, uint32_t* gbits,
+                           const uint32_t* __restrict__ gx) {
   const uint32_t w0 = B0 >> 5, w1 = (B1 - 1) >> 5;
+  const uint32_t R = uf_find_ro(uf, anchor);
+  const uint32_t X = gbits ? *gx : INV;
+  const bool set_g = X != INV && uf_find_ro(uf, X) == R;
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
        w += gridDim.x * blockDim.x) {
     uint32_t bits = word_in(bitmap, w, B0, B1);
     if (!bits) continue;
+    if (set_g) atomicOr(&gbits[w], bits);
     uint32_t cur = (w << 5) + __ffs(bits) - 1;
     const uint32_t first = cur;
+    uf[cur] = R;
     bits &= bits - 1;
     while (bits) {
       uint32_t nx = (w << 5) + __ffs(bits) - 1;
       bits &= bits - 1;
       parent[cur] = nx;
+      uf[nx] = R;
       cur = nx;
     }
     for (uint32_t v = w + 1, k = 0; v <= w1 && k < limit; ++v, ++k) {
@@ -2229,36 +2245,11 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   }
 }
 
-// Giant fold (before k_kb_union): every marked rank of the bucket ends in the anchor's
-// component (the spine joins all of them to G), and its union-find slot is still its own
-// (iota: nothing links an in-bucket rank before its bucket's union), so it is stored under
-// that component's root R directly — no find, no CAS.  k_kb_union then skips the links
-// between two marked ranks (already in one tree).
-// gbits (nullable): the marked ranks are giant members; when the bitmap's reference vertex
-// *gx lies in the anchor's component they are set there too (see k_kb_map).
-__global__ void k_kb_fold(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
-                          uint32_t* uf, uint32_t anchor, uint32_t* gbits,
-                          const uint32_t* __restrict__ gx) {
-  const uint32_t R = uf_find_ro(uf, anchor);
-  const uint32_t X = gbits ? *gx : INV;
-  const bool set_g = X != INV && uf_find_ro(uf, X) == R;
-  for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w <= ((B1 - 1) >> 5);
-       w += gridDim.x * blockDim.x) {
-    uint32_t bits = word_in(bitmap, w, B0, B1);
-    if (set_g && bits) atomicOr(&gbits[w], bits);
-    while (bits) {
-      const uint32_t v = (w << 5) + __ffs(bits) - 1;
-      bits &= bits - 1;
-      uf[v] = R;
-    }
-  }
-}
-
 // anchor: rank B0 - 1 (INV for the first bucket).  Its root R is never linked below another
 // root here, so the giant keeps one root from bucket to bucket: the map of the next bucket,
 // which runs concurrently in the pipelined loop, finds the same R from the same rank.  (All
 // threads read the same R: no union of this launch can move it.)
-// FOLD: k_kb_fold ran; links between two marked ranks are skipped, and the marks are cleared
+// FOLD: the giant fold ran (k_kb_spine); links between two marked ranks are skipped, and the marks are cleared
 // by k_kb_label instead (this launch reads them).
 template <bool FOLD>
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
@@ -2413,9 +2404,10 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                          uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx);
-    if (anchor != INV)
+    if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
-                         0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit);
+                         0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
+                         uf, anchor, gbits, gx);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
     const uint32_t qchunk = 64;  // zipper queue: edges per wave refill
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
@@ -2425,10 +2417,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   }
   // giant fold: the marks are relative to the anchor's component; its root R_a may later be
   // linked below the union's R (pipelined: different anchors) — the folded ranks follow it
-  const bool fold = nonempty && anchor != INV && B1 > B0;
-  if (fold)
-    hipLaunchKernelGGL(k_kb_fold, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
-                       0, s, (const uint32_t*)bitmap, B0, B1, uf, anchor, gbits, gx);
+  const bool fold = nonempty && anchor != INV && B1 > B0;  // done by k_kb_spine
   // the linked pre-bucket roots (device count) can outnumber the bucket's ranks many times
   // over (hub buckets: ~500 ranks, ~0.3 M linked roots): a full grid, whatever the width
   unsigned ug = MAX_GRID;
