@@ -126,6 +126,11 @@ PATCHES = {
     "zipplain": [("  if (LOAD == 0) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);", "  if (LOAD == 0) return *(volatile uint32_t*)p;")],
     # zipper: no jump-hint load on the first step of a pending edge (most edges take one step)
     "zipj2": [("    if (JUMP) {\n      const uint32_t j = jump[s.x];", "    if (JUMP && !(s.x == s.a && s.prev == INV)) {\n      const uint32_t j = jump[s.x];")],
+    # zipper grid / queue chunk
+    "zg512": [("    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept,", "    hipLaunchKernelGGL(zk, dim3(512), dim3(BLOCK), 0, s, kept,")],
+    "zg1024": [("    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept,", "    hipLaunchKernelGGL(zk, dim3(1024), dim3(BLOCK), 0, s, kept,")],
+    "zq64": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 64;")],
+    "zq512": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 512;")],
 }
 CAPI_PATCHES = {
     "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],

@@ -2409,7 +2409,10 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
                          uf, anchor, gbits, gx);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
-    const uint32_t qchunk = 64;  // zipper queue: edges per wave refill
+    // zipper queue: edges per wave refill (tree phase, RMAT-26: 26.3 / 25.6 / 25.3 / 25.8 ms at
+    // 64 / 256 / 512 / 1024; twitter-shape: 37.7 / 37.6 / 38.9 ms at 64 / 256 / 512; LJ-shape
+    // within noise)
+    const uint32_t qchunk = 256;
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
