@@ -1602,6 +1602,12 @@ struct ZRec {  // where to record pre-bucket roots (x < B0) that a CAS links for
   uint32_t B0 = 0;
   uint32_t* linked = nullptr;
   uint32_t* n_linked = nullptr;
+  // block-local staging (LDS, nullable): appends reserve here with LDS atomics and the block
+  // flushes once at its end (zip_flush_linked) — one global counter hit by every wave at
+  // every step serialises (~88 returning atomics per microsecond on one word)
+  uint32_t* lbuf = nullptr;
+  uint32_t* lcnt = nullptr;
+  uint32_t lcap = 0;
 };
 
 // The giant's spine inside a kb bucket [B0, B1).  G is the elimination-tree root of the
@@ -1805,10 +1811,27 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
       const uint64_t bal = __ballot(linked);
       if (bal) {
         const int leader = __ffsll((unsigned long long)bal) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(rec.n_linked, (uint32_t)__popcll(bal));
-        base = __builtin_amdgcn_readlane(base, leader);
-        if (linked) rec.linked[base + __popcll(bal & lt)] = s.x;
+        const uint32_t cnt = (uint32_t)__popcll(bal), r = (uint32_t)__popcll(bal & lt);
+        if (rec.lbuf) {  // the block's LDS buffer; what does not fit goes straight out
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(rec.lcnt, cnt);
+          base = __builtin_amdgcn_readlane(base, leader);
+          const uint32_t over0 = base > rec.lcap ? base : rec.lcap;
+          const uint32_t nover = base + cnt > over0 ? base + cnt - over0 : 0u;
+          uint32_t g = 0;
+          if (nover && lane == leader) g = atomicAdd(rec.n_linked, nover);
+          g = __builtin_amdgcn_readlane(g, leader);
+          if (linked) {
+            const uint32_t slot = base + r;
+            if (slot < rec.lcap) rec.lbuf[slot] = s.x;
+            else rec.linked[g + (slot - over0)] = s.x;
+          }
+        } else {
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(rec.n_linked, cnt);
+          base = __builtin_amdgcn_readlane(base, leader);
+          if (linked) rec.linked[base + r] = s.x;
+        }
       }
     }
   }
@@ -2223,10 +2246,18 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
                          uint32_t* jump, unsigned long long* stats, uint32_t* linked,
                          uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
                          uint32_t qchunk) {
+  constexpr uint32_t LCAP = 2048;
+  __shared__ uint32_t lbuf[LCAP];
+  __shared__ uint32_t lcnt, lbase;
+  if (threadIdx.x == 0) lcnt = 0;
+  __syncthreads();
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
   rec.n_linked = n_linked;
+  rec.lbuf = lbuf;
+  rec.lcnt = &lcnt;
+  rec.lcap = LCAP;
   EdgeSrc src{kept};
   const uint64_t nk = *n_kept;
   if (anchor != INV) {
@@ -2243,6 +2274,12 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   } else {
     tree_queue_body<0, 1, STATS, true, false>(src, nk, parent, jump, stats, rec, qchunk);
   }
+  // the block's staged linked roots: one reservation, a coalesced copy
+  __syncthreads();
+  const uint32_t n = min(lcnt, LCAP);
+  if (threadIdx.x == 0) lbase = n ? atomicAdd(n_linked, n) : 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) linked[lbase + i] = lbuf[i];
 }
 
 // anchor: rank B0 - 1 (INV for the first bucket).  Its root R is never linked below another
