@@ -131,8 +131,27 @@ PATCHES = {
     "zg1024": [("    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept,", "    hipLaunchKernelGGL(zk, dim3(1024), dim3(BLOCK), 0, s, kept,")],
     "zq64": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 64;")],
     "zq512": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 512;")],
+    # ---- front-half ablations (timing only; use with +front so the tree never runs) ----
+    # degree scatter without the write-out of the staged runs
+    "dsnw": [("    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];", "")],
+    # degree scatter: LDS atomics only (no staging stores, no write-out)
+    "dsatom": [("      buf[atomicAdd(&cur[e.x >> SH], 1u)] = (uint16_t)(e.x & lmask);\n      if (file_mode || !loop) buf[atomicAdd(&cur[e.y >> SH], 1u)] = (uint16_t)(e.y & lmask);",
+                "      atomicAdd(&cur[e.x >> SH], 1u);\n      if (file_mode || !loop) atomicAdd(&cur[e.y >> SH], 1u);"),
+               ("    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];", "")],
+    # hist16 without the LDS adds (loads + unpack only)
+    "h16load": [("            if (!done) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));\n            continue;",
+                 "            if (!done) acc[0] += v;\n            continue;")],
+    # second partition pass without the rank gather (ry = y / 4: in range at RMAT-26)
+    "p1ng": [("      ry[k] = (x != y && y < n_rank) ? rank[y] : INV;", "      ry[k] = y >> 2;")],
+    # edge pass without the rank gather
+    "epng": [("      rx[k] = (e[k].y != RY_SELF && e[k].x < n_rank) ? rank[e[k].x] : INV;", "      rx[k] = e[k].x >> 2;")],
+    # bin scatter without the write-out
+    "bsnw": [("    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];", "")],
+    "front": [],
 }
 CAPI_PATCHES = {
+    "front": [('    if (tm) tm->mark("edge_pass");\n    HIP_CHECK(hipEventSynchronize(c.bins_ev));',
+               '    if (tm) tm->mark("edge_pass");\n    HIP_CHECK(hipEventSynchronize(c.bins_ev));\n    HIP_CHECK(hipStreamSynchronize(s));\n    if (tm) tm->mark("bin_scatter");\n    return;')],
     "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],
 }
 
@@ -141,7 +160,7 @@ def main():
     name = sys.argv[1]
     text = open(os.path.join(SRC, "sheep_kernels.hip")).read()
     for part in name.split("+"):
-        for a, b in PATCHES[part]:
+        for a, b in PATCHES.get(part, []):
             assert a in text, a
             text = text.replace(a, b)
     capi = open(os.path.join(SRC, "sheep_capi.cpp")).read()
@@ -149,9 +168,10 @@ def main():
         a = 'h[0], h[5], h[7], h[8], h[9], h[10], h[11], h[12]);'
         assert a in capi
         capi = capi.replace(a, a + '\n    fprintf(stderr, "map_phases_cycles load+bits %llu finds %llu label %llu lds %llu barA %llu flush %llu compact+barB+write %llu\\n", h[1], h[2], h[3], h[4], h[13], h[14], h[15]);')
-    for a, b in CAPI_PATCHES.get(name, []):
-        assert a in capi, a
-        capi = capi.replace(a, b)
+    for part in name.split("+"):
+        for a, b in CAPI_PATCHES.get(part, []):
+            assert a in capi, a
+            capi = capi.replace(a, b)
     tmp = "/tmp/sheep_lab_%s" % name
     os.makedirs(tmp, exist_ok=True)
     for f in ("powerlaw.h", "rmat.h", "sheep_internal.h", "sheep_comm.h"):

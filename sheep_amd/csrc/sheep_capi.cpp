@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <memory>
 #include <chrono>
 #include <mutex>
@@ -45,6 +46,7 @@ static const KnobDef kKnobs[] = {
     {"degb_plain", &Knobs::degb_plain},   {"degb_hist", &Knobs::degb_hist16},
     {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
+    {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
 };
 
 static Knobs g_knobs;
@@ -367,11 +369,19 @@ static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 
   *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
 }
 
+// Directly binned records (launch_edge_bin): the buckets' .second are bin indices, bucket k's
+// records are the filled parts of bins [bk[k].second, bk[k+1].second).
+struct SegPlan {
+  KbSegs dev{};                       // device start / cursor / capacity-end arrays
+  std::vector<unsigned long long> cstart;  // host: capacity start of each bin, then the end
+};
+
 static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, uint64_t m,
                              uint32_t n_seq, int lo_bit, uint32_t* d_parent, uint32_t* jump,
                              uint32_t* hcnt, bool stats, unsigned long long* ws, hipStream_t s,
                              Timer* tm, const Buckets* given = nullptr,
-                             const uint32_t* bins = nullptr, uint32_t nb = 0) {
+                             const uint32_t* bins = nullptr, uint32_t nb = 0,
+                             const SegPlan* seg = nullptr) {
   uint32_t K_e, K_r;
   kb_counts(m, &K_e, &K_r);
   uint32_t K = K_e + K_r;
@@ -421,8 +431,13 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // on s, with kept pairs, marks and counters double-buffered by bucket parity — each needs
   // half of the buffer.  The map of bucket k+1 anchors the giant at the last rank of bucket
   // k-1 (launch_kb_map).
+  // records of bucket k (at most: the capacity of its bins when directly binned)
+  auto recs = [&](size_t k) -> uint64_t {
+    return seg ? seg->cstart[bk[k + 1].second] - seg->cstart[bk[k].second]
+               : bk[k + 1].second - bk[k].second;
+  };
   uint64_t max_e = 0;
-  for (size_t k = 0; k < nbk; ++k) max_e = std::max<uint64_t>(max_e, bk[k + 1].second - bk[k].second);
+  for (size_t k = 0; k < nbk; ++k) max_e = std::max<uint64_t>(max_e, recs(k));
   const bool per_bucket = knobs().tree_stats == 2;
   const bool pipe = knobs().kb_pipe && !per_bucket && 2 * max_e <= m;
   uint64_t* kept[2] = {spare, pipe ? spare + m / 2 : spare};
@@ -446,14 +461,22 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   auto map_k = [&](size_t k, hipStream_t st) {
     int p = par(k);
     size_t sp = tm ? tm->span_begin("kb_map", st) : 0;
-    launch_kb_map(sorted, bk[k].second, bk[k + 1].second, bk[k].first, anchor_of(k), uf, label,
-                  kept[p], bitmaps + p * bm_words, counters + p * 16, lo_bit, hcnt, stats, ws,
-                  bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer, st);
+    KbSegs sg{};
+    if (seg) {
+      sg = seg->dev;
+      sg.i0 = (uint32_t)bk[k].second;
+      sg.i1 = (uint32_t)bk[k + 1].second;
+    }
+    launch_kb_map(sorted, seg ? seg->cstart[bk[k].second] : bk[k].second,
+                  seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
+                  anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
+                  lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer,
+                  st, seg ? &sg : nullptr);
     if (tm) tm->span_end(sp, st);
   };
   auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
     int p = par(k);
-    launch_kb_apply(bk[k + 1].second > bk[k].second, bk[k].first, bk[k + 1].first, anchor_of(k),
+    launch_kb_apply(recs(k) > 0, bk[k].first, bk[k + 1].first, anchor_of(k),
                     uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
                     spqs + p * spq_words, counters + p * 16, defer || (pipe && knobs().kb_refresh), stats,
                     ws, gbits, gbits ? gx + (slot & 1) : nullptr, st);
@@ -511,7 +534,9 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
 // as dsum(c) * (D_c + dsum(c)/2) / total, D_c the degree mass of the chunks below.  A bin
 // closes at 1/320 of the estimated records, or when 32K ranks wide (the kb map's LDS window)
 // unless it holds almost nothing; at most 511 bins, then the INVALID bin (bound n_seq).
-static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32_t n_seq) {
+// est (nullable): the estimated records of each bin but the last (the INVALID bin).
+static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32_t n_seq,
+                                       std::vector<double>* est = nullptr) {
   const size_t nch = dsum.size();
   std::vector<double> w(nch);
   double tot = 0, D = 0, W = 0;
@@ -522,8 +547,20 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
     W += w[c];
   }
   std::vector<uint32_t> b;
+  // the estimate of bins [b[i], b[i+1]) (chunk-aligned bounds, the last one n_seq)
+  auto estimate = [&](const std::vector<uint32_t>& bb) {
+    if (!est) return;
+    est->assign(bb.size() - 1, 0.0);
+    for (size_t i = 0; i + 1 < bb.size(); ++i)
+      for (size_t c = bb[i] / 256; c < std::min<size_t>(nch, ((size_t)bb[i + 1] + 255) / 256); ++c)
+        (*est)[i] += w[c];
+  };
   // No estimated records (every record a self-loop, or no degrees): one bin holds them all.
-  if (!(tot > 0) || !(W > 0) || nch < 2) return {0u, n_seq};
+  if (!(tot > 0) || !(W > 0) || nch < 2) {
+    std::vector<uint32_t> one = {0u, n_seq};
+    if (est) est->assign(1, (double)W);
+    return one;
+  }
   double wmax = W / 320, wide = W / 50000;
   for (int attempt = 0; attempt < 32; ++attempt) {
     b.assign(1, 0u);
@@ -550,6 +587,7 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
   }
   b.push_back(n_seq);
   if (b.size() > 512) throw ApiError(-EIO, "make_bins: more than 512 hi bins");
+  estimate(b);
   return b;
 }
 
@@ -593,9 +631,12 @@ static Buckets buckets_from_bins(const std::vector<uint32_t>& bounds,
   return bk;
 }
 
+// allow_direct: the hi bins may be filled directly by the edge pass (launch_edge_bin); false
+// after a bin outgrew its estimate (the records are then grouped by the scatter).
 static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                            uint32_t n_rank, uint32_t n_seq, uint32_t* d_parent, uint32_t* d_pst,
-                           hipStream_t s, Timer* tm, const DegInfo* di = nullptr) {
+                           hipStream_t s, Timer* tm, const DegInfo* di = nullptr,
+                           bool allow_direct = true) {
   require_records(m, "tree build");
   if (n_seq == 0) return;
   launch_fill(d_parent, INV, n_seq, s);
@@ -654,7 +695,56 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   Buckets given;
   const uint32_t* dbins = nullptr;
   uint32_t nbins = 0;
-  if (use_bins) {
+  SegPlan plan;
+  const bool direct = use_bins && allow_direct && knobs().bin_direct;
+  uint32_t* ovf = c.d_err + 1;  // a directly binned bin outgrew its capacity
+  if (direct) {
+    // Each bin gets a capacity region sized by its estimated records (+ slack); the edge pass
+    // fills them directly, and the buckets are cut on the estimate (any cuts are exact).
+    HIP_CHECK(hipEventSynchronize(c.bins_ev));
+    std::vector<uint64_t> hd(c.h_chunks, c.h_chunks + nch);
+    std::vector<double> est;
+    std::vector<uint32_t> bounds = make_bins(hd, n_seq, &est);
+    nbins = (uint32_t)bounds.size();
+    uint32_t* db = (uint32_t*)c.scratch.get("hi_bins", 512 * 4);
+    HIP_CHECK(hipMemcpyAsync(db, bounds.data(), nbins * 4, hipMemcpyHostToDevice, s));
+    dbins = db;
+    const double slack = 1.0 + knobs().bin_slack / 1000.0;
+    plan.cstart.assign(nbins, 0ull);
+    std::vector<unsigned long long> h(3 * 512, 0ull);  // start | cursor | capacity end
+    for (uint32_t i = 0; i + 1 < nbins; ++i) {
+      const uint64_t cap = (uint64_t)std::ceil(est[i] * slack) + 8192;
+      plan.cstart[i + 1] = plan.cstart[i] + cap;
+      h[i] = h[512 + i] = plan.cstart[i];
+      h[1024 + i] = plan.cstart[i + 1];
+    }
+    unsigned long long* dseg = (unsigned long long*)c.scratch.get("bin_segs", h.size() * 8);
+    HIP_CHECK(hipMemcpyAsync(dseg, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemsetAsync(ovf, 0, 4, s));
+    uint64_t* binned = (uint64_t*)c.scratch.get(
+        "e_binned", std::max<uint64_t>(plan.cstart[nbins - 1], 1) * 8);
+    launch_edge_bin(src, part, m, d_rank, n_rank, c.d_err, db, nbins, dseg + 512, dseg + 1024,
+                    binned, ovf, s);
+    if (tm) tm->mark("edge_pass");
+    // One readback before the kb loop is enqueued (the host then enqueues while the GPU runs
+    // the first buckets): a bin that outgrew its estimate holds a hole where its dropped runs
+    // were reserved, so the records are grouped again through the scatter.
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 8, ovf, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c.h_pinned[8]) {
+      DegInfo d2 = *di;
+      d2.part_first_done = false;  // k_part's passes are run again from d_uv
+      d2.yhist_ready = false;      // the first partition consumed the y-digit counts
+      build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, tm, &d2, false);
+      return;
+    }
+    plan.dev = {dseg, dseg + 512, dseg + 1024, 0u, 0u};
+    given.emplace_back(0u, 0ull);
+    for (uint32_t i : bucket_cuts(bounds, plan.cstart, m, n_seq)) given.emplace_back(bounds[i], i);
+    given.emplace_back(n_seq, (uint64_t)(nbins - 1));
+    sorted = binned;
+    spare = items;  // free: held k_part's mid records (src is items_b or d_uv)
+  } else if (use_bins) {
     HIP_CHECK(hipEventSynchronize(c.bins_ev));
     std::vector<uint64_t> hd(c.h_chunks, c.h_chunks + nch);
     std::vector<uint32_t> bounds = make_bins(hd, n_seq);
@@ -688,7 +778,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   }
   unsigned long long* ws = (unsigned long long*)c.scratch.get("tree_ws", 64 * 2);
   tree_from_sorted(c, sorted, spare, m, n_seq, lo_bit, d_parent, jump, hcnt, stats, ws, s, tm,
-                   use_bins ? &given : nullptr, dbins, nbins);
+                   use_bins ? &given : nullptr, dbins, nbins, direct ? &plan : nullptr);
   if (tm) tm->mark("tree_insert");
   if (pst_count) {
     launch_pst_from_count(di->seq, n_seq, di->deg, di->selfc, di->mode, hcnt, d_pst, s, di->nsd);

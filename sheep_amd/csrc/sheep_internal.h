@@ -50,6 +50,8 @@ struct Knobs {
   int bin_scatter = 1;   // SHEEP_BIN_SCATTER: unstable 16K-item bin scatter (0: stable radix scatter)
   int ep_plain = 1;      // SHEEP_EP_PLAIN: edge pass counts bins with plain LDS atomics
   int tree_stats = 0;    // SHEEP_TREE_STATS: 1 totals, 2 per bucket (stderr; diagnostics)
+  int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
+  int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
 };
 Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
 
@@ -165,6 +167,21 @@ void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* 
                            const uint32_t* nsd = nullptr);
 void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t K_r,
                       uint32_t n_seq, int gshift, unsigned long long* out, hipStream_t s);
+// The records of a kb bucket when they were binned directly (launch_edge_bin): bins [i0, i1),
+// bin i's items at [start[i], min(cur[i], cap[i])) (device arrays).
+struct KbSegs {
+  const unsigned long long* start;
+  const unsigned long long* cur;
+  const unsigned long long* cap;
+  uint32_t i0, i1;
+};
+// Direct binning (sheep_kernels.hip): records (uv, or k_part's pre records) -> items grouped by
+// hi bin, each bin in its capacity region [cursor[b] at entry, cap_end[b]); cursor[b] ends at
+// the bin's fill.  *ovf is set (and the run dropped) when a bin overflows its capacity.
+void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
+                     uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                     unsigned long long* cursor, const unsigned long long* cap_end, uint64_t* out,
+                     uint32_t* ovf, hipStream_t s);
 // One kb bucket in two halves (sheep_kernels.hip): the map (records -> kept pairs + giant marks
 // + hi counts) and the apply (spine, zipper, union-find fold, labels).  counters: this
 // bucket parity's 4 words; anchor: see launch_kb_map.
@@ -176,7 +193,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,
                    const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
                    bool defer /* misses kept as (b, a) for launch_kb_apply's refresh */,
-                   hipStream_t s);
+                   hipStream_t s, const KbSegs* segs = nullptr);
 // Before a map (nothing else touching the union-find): keep the giant bitmap's reference
 // vertex (*gx_rd) if it is in the anchor's component, else move it to the anchor and clear
 // the bitmap (n_seq / 32 + 2 words); the result goes to *gx_wr.

@@ -1383,6 +1383,125 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 }
 
 // ---------------------------------------------------------------------------------------
+// Direct binning: the edge pass stores its items straight into their hi bins, so the items
+// are written once and there is no scatter pass (no digits array, no tile count matrix).
+// Bin b owns the capacity region [cursor0[b], cap_end[b]) of `out`, sized by the host from the
+// degree estimate of its records (make_bins; the estimate is within a few % on R-MAT and
+// Chung-Lu inputs); a tile reserves its run of bin b with one atomic on cursor[b] (which then
+// ends at the bin's fill).  A run that would cross cap_end[b] is dropped and *ovf set: the
+// caller then groups the records again through the scatter path.  Records without a tree
+// item (self-loops, INVALID hi) are not stored.  Tile = NT threads x IT records, staged in LDS
+// in bin order and written as whole runs per wave (as k_bin_scatter).
+// ---------------------------------------------------------------------------------------
+template <bool PRE, int NT, int IT>
+__global__ void __launch_bounds__(NT)
+k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
+           uint32_t n_rank, uint32_t* err, const uint32_t* __restrict__ bins, uint32_t nb,
+           unsigned long long* cursor, const unsigned long long* __restrict__ cap_end,
+           uint64_t* __restrict__ out, uint32_t* ovf) {
+  static_assert(NT >= 512, "one thread per bin in the scan");
+  constexpr int TILE = NT * IT;
+  __shared__ uint64_t stage[TILE];
+  __shared__ uint32_t hist[512], tstart[512], sb[512], wsum[NT / 64];
+  __shared__ unsigned long long gbase[512];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
+  if (t < 512) hist[t] = 0;
+  for (uint32_t i = t; i < nb; i += NT) sb[i] = bins[i];
+  uint2 e[IT];
+  uint32_t rx[IT], ry[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const uint32_t j = (uint32_t)k * NT + t;
+    e[k] = j < tile_n ? uv[tbase + j] : make_uint2(0, PRE ? RY_SELF : 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {  // every gather issued before any is used
+    if (PRE) {
+      rx[k] = (e[k].y != RY_SELF && e[k].x < n_rank) ? rank[e[k].x] : INV;
+    } else {
+      const bool g = e[k].x != e[k].y;
+      rx[k] = (g && e[k].x < n_rank) ? rank[e[k].x] : INV;
+      ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
+    }
+  }
+  __syncthreads();
+  uint64_t item[IT];
+  uint32_t pk[IT];  // bin << 16 | index within the tile's run of the bin; ~0u: not stored
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const bool loop = PRE ? e[k].y == RY_SELF : e[k].x == e[k].y;
+    uint32_t hi = INV, lo = INV;
+    pk[k] = ~0u;
+    if ((uint32_t)k * NT + t < tile_n && !loop) {  // insert's edge loop, jtree.cpp:73-90
+      const bool ox = e[k].x >= n_rank;
+      bool oy;
+      uint32_t r_y;
+      if (PRE) { oy = e[k].y == RY_OUT; r_y = oy ? INV : e[k].y; }
+      else { oy = e[k].y >= n_rank; r_y = ry[k]; }
+      if ((ox && r_y != INV) || (oy && rx[k] != INV)) {
+        atomicOr(err, ERR_RANGE);
+      } else {
+        lo = min(rx[k], r_y);
+        hi = max(rx[k], r_y);
+      }
+    }
+    item[k] = ((uint64_t)hi << 32) | lo;
+    if (hi != INV) {
+      const uint32_t d = bin_of(sb, nb, hi);
+      pk[k] = (d << 16) | atomicAdd(&hist[d], 1u);
+    }
+  }
+  __syncthreads();
+  if (t < 512) {
+    const uint32_t c = hist[t];
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[w] = incl;
+    tstart[t] = incl - c;
+    unsigned long long g = ~0ull;
+    if (c) {
+      g = atomicAdd(&cursor[t], (unsigned long long)c);
+      if (g + c > cap_end[t]) {
+        atomicOr(ovf, 1u);
+        g = ~0ull;
+      }
+    }
+    gbase[t] = g;
+  }
+  __syncthreads();
+  if (t < 512) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    tstart[t] += add;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IT; ++k)
+    if (pk[k] != ~0u) stage[tstart[pk[k] >> 16] + (pk[k] & 0xFFFFu)] = item[k];
+  __syncthreads();
+  for (uint32_t d = w; d < 512; d += NT / 64) {
+    const uint32_t c = hist[d];
+    const unsigned long long g = gbase[d];
+    if (c == 0 || g == ~0ull) continue;
+    const uint32_t s0 = tstart[d];
+    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];
+  }
+}
+
+void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
+                     uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
+                     unsigned long long* cursor, const unsigned long long* cap_end, uint64_t* out,
+                     uint32_t* ovf, hipStream_t s) {
+  if (m == 0) return;
+  constexpr int NT = 512, IT = 16;  // 8192-record tiles, 64 KB stage: two blocks per CU
+  const unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
+  auto k = pre ? k_edge_bin<true, NT, IT> : k_edge_bin<false, NT, IT>;
+  hipLaunchKernelGGL(k, dim3(nt), dim3(NT), 0, s, (const uint2*)uv, m, rank, n_rank, err, bins, nb,
+                     cursor, cap_end, out, ovf);
+}
+
+// ---------------------------------------------------------------------------------------
 // Partitioned rank gathers.  rank[] (4 B per id, 268 MB at RMAT-26) is far beyond L2 and the
 // stream evicts it from the Infinity Cache: gathered in stream order, every lookup is a 64-B
 // HBM access (~60 G lookups/s, 2 per record).  Partitioned by the looked-up id's top 8 bits,
@@ -1929,8 +2048,8 @@ static constexpr uint32_t KM_FLUSH = 65535 / KM_CHUNK;  // chunks per window flu
 
 template <bool STATS>
 __global__ void __launch_bounds__(KM_THREADS)
-k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
-         int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
+k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, KbSegs sg,
+         uint32_t B0, int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
          const uint32_t* __restrict__ gx, int defer) {
@@ -1938,6 +2057,8 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
   __shared__ uint32_t sbins[512];
+  __shared__ unsigned long long s_s0[512], s_s1[512];  // the bucket's segments [s0, s1)
+  __shared__ uint32_t s_cp[513];                        // chunks before each segment
   constexpr int R = KM_R;
   // RG: the giant's union-find root, found from the anchor rank (see launch_kb_map); it does
   // not move while this map runs (k_kb_union links everything else below it).  Membership is
@@ -1959,10 +2080,36 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
   // Each block maps a contiguous run of chunks, so that consecutive chunks mostly share one
   // window (a bin): the window is flushed to global memory only when the next chunk's differs,
   // after KM_FLUSH chunks (the packed 16-bit counts must not carry), and at the end.
-  const uint64_t total = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
-  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
-  const uint64_t cb = e_begin + (uint64_t)blockIdx.x * per * KM_CHUNK;
-  const uint64_t ce = min(cb + per * KM_CHUNK, e_end);
+  // The bucket's records: one range [e_begin, e_end), or the filled part of each of its
+  // directly binned bins (launch_edge_bin) — chunks never cross a segment end.
+  uint32_t nseg = 1;
+  if (sg.start) {
+    nseg = sg.i1 - sg.i0;
+    for (uint32_t i = t; i < nseg; i += KM_THREADS) {
+      s_s0[i] = sg.start[sg.i0 + i];
+      s_s1[i] = min(sg.cur[sg.i0 + i], sg.cap[sg.i0 + i]);
+    }
+  } else if (t == 0) {
+    s_s0[0] = e_begin;
+    s_s1[0] = e_end;
+  }
+  __syncthreads();
+  if (w == 0) {
+    uint32_t run = 0;
+    for (uint32_t b0 = 0; b0 < nseg; b0 += 64) {
+      const uint32_t i = b0 + lane;
+      const uint32_t c = i < nseg ? (uint32_t)((s_s1[i] - s_s0[i] + KM_CHUNK - 1) / KM_CHUNK) : 0u;
+      const uint32_t incl = wave_incl_scan(c);
+      if (i < nseg) s_cp[i] = run + incl - c;
+      run += (uint32_t)__shfl((int)incl, 63);
+    }
+    if (lane == 0) s_cp[nseg] = run;
+  }
+  __syncthreads();
+  const uint32_t total = s_cp[nseg];
+  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint32_t j0 = min(blockIdx.x * per, total), j1 = min(j0 + per, total);
+  uint32_t si = 0;  // segment of the chunk fetched last (chunks are visited in order)
   auto window = [&](uint32_t h0, uint32_t blast, uint32_t& bbase, uint32_t& gend) {
     if (bins) {
       bbase = sbins[bin_of(sbins, nb, h0)] & ~31u;
@@ -1977,20 +2124,23 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
   // chunk c0's records (and its first / last hi) are loaded one chunk ahead
   uint64_t nx[R];
   uint32_t nh0 = 0, nbl = 0;
-  auto fetch = [&](uint64_t c0) {
-    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, ce);
+  uint64_t nc0 = 0, nc1 = 0;
+  auto fetch = [&](uint32_t j) {
+    while (s_cp[si + 1] <= j) ++si;
+    nc0 = s_s0[si] + (uint64_t)(j - s_cp[si]) * KM_CHUNK;
+    nc1 = min(nc0 + (uint64_t)KM_CHUNK, s_s1[si]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint64_t idx = c0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
-      nx[r] = idx < c1 ? items[idx] : 0ull;
+      const uint64_t idx = nc0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
+      nx[r] = idx < nc1 ? items[idx] : 0ull;
     }
-    nh0 = (uint32_t)(items[c0] >> 32);
-    nbl = (uint32_t)(items[c1 - 1] >> 32);
+    nh0 = (uint32_t)(items[nc0] >> 32);
+    nbl = (uint32_t)(items[nc1 - 1] >> 32);
   };
-  if (cb < ce) fetch(cb);
+  if (j0 < j1) fetch(j0);
   uint32_t since_flush = 0;
-  for (uint64_t c0 = cb; c0 < ce; c0 += KM_CHUNK) {
-    const uint64_t c1 = min(c0 + (uint64_t)KM_CHUNK, ce);
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint64_t c0 = nc0, c1 = nc1;
     uint64_t it[R];
     uint32_t vmask = 0;
 #pragma unroll
@@ -2009,8 +2159,8 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, u
       const uint32_t a = (uint32_t)it[r];
       gw[r] = (use_bm && ((vmask >> r) & 1) && a < B0) ? gbits[a >> 5] : 0u;
     }
-    const bool more = c0 + KM_CHUNK < ce;
-    if (more) fetch(c0 + KM_CHUNK);  // issued after the bitmap loads
+    const bool more = j + 1 < j1;
+    if (more) fetch(j + 1);  // issued after the bitmap loads
     uint32_t giant = 0, miss = 0, x[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -2407,15 +2557,21 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
-                   const uint32_t* gx, bool defer, hipStream_t s) {
+                   const uint32_t* gx, bool defer, hipStream_t s, const KbSegs* segs) {
+  // segs: e_begin / e_end bound the bucket's records (the capacity of its bins)
   if (e_end <= e_begin) return;
+  KbSegs sg{};
+  if (segs) {
+    sg = *segs;
+    if (sg.i1 <= sg.i0 || sg.i1 - sg.i0 > 512) return;
+  }
   uint64_t chunks = (e_end - e_begin + KM_CHUNK - 1) / KM_CHUNK;
   // One block per CU: the apply of the previous bucket (the loop's critical path) runs beside
   // this map, and more map blocks slow it down more than they speed the map up (RMAT-26 tree
   // phase 28.6 / 27.6 / 31.0 / 29.8 ms at 512 / 256 / 320 / 384 blocks; 192: 29.7).
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-  hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, B0, gshift,
+  hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, sg, B0, gshift,
                      uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
                      gx ? gbits : nullptr, gx, (int)defer);
 }

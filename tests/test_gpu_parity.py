@@ -84,10 +84,14 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
     (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
     (16, 23, 0, {"edge_part": 1}),  # the partitioned gathers at a small size
+    (18, 24, 0, {"bin_slack": -900}),       # direct bins at 1/10 of the estimate: they overflow
+                                            # and the records are grouped again by the scatter
+    (16, 25, 0, {"bin_slack": -900, "edge_part": 0}),  # the same from unpartitioned records
+    (17, 26, 0, {"bin_direct": 0}),         # edge pass + bin scatter (no direct binning)
     (16, 24, 0, {"edge_part": 0}),  # direct gathers, hi bins
     (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
-    (18, 29, 0, {"bin_scatter": 0}),  # stable bin scatter
+    (18, 29, 0, {"bin_scatter": 0, "bin_direct": 0}),  # stable bin scatter
 ])
 def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
