@@ -131,23 +131,17 @@ PATCHES = {
     "zg1024": [("    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept,", "    hipLaunchKernelGGL(zk, dim3(1024), dim3(BLOCK), 0, s, kept,")],
     "zq64": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 64;")],
     "zq512": [("    const uint32_t qchunk = 256;", "    const uint32_t qchunk = 512;")],
-    # ---- front-half ablations (timing only; use with +front so the tree never runs) ----
-    # degree scatter without the write-out of the staged runs
-    "dsnw": [("    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];", "")],
-    # degree scatter: LDS atomics only (no staging stores, no write-out)
-    "dsatom": [("      buf[atomicAdd(&cur[e.x >> SH], 1u)] = (uint16_t)(e.x & lmask);\n      if (file_mode || !loop) buf[atomicAdd(&cur[e.y >> SH], 1u)] = (uint16_t)(e.y & lmask);",
-                "      atomicAdd(&cur[e.x >> SH], 1u);\n      if (file_mode || !loop) atomicAdd(&cur[e.y >> SH], 1u);"),
-               ("    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];", "")],
-    # hist16 without the LDS adds (loads + unpack only)
-    "h16load": [("            if (!done) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));\n            continue;",
-                 "            if (!done) acc[0] += v;\n            continue;")],
-    # second partition pass without the rank gather (ry = y / 4: in range at RMAT-26)
-    "p1ng": [("      ry[k] = (x != y && y < n_rank) ? rank[y] : INV;", "      ry[k] = y >> 2;")],
-    # edge pass without the rank gather
-    "epng": [("      rx[k] = (e[k].y != RY_SELF && e[k].x < n_rank) ? rank[e[k].x] : INV;", "      rx[k] = e[k].x >> 2;")],
-    # bin scatter without the write-out
-    "bsnw": [("    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];", "")],
+    # (timing-only ablations that leave buffers unwritten are NOT safe: one of them hung and
+    # faulted the GPU — garbage ids reach kernels that index with them.  Keep variants exact.)
     "front": [],
+    "p1k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
+              "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 1024;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = 8;")],
+    "p0k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
+              "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = 8, PT1_ITEMS = PT_ITEMS;")],
+    "p01k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
+               "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 1024;\nstatic constexpr int PT0_ITEMS = 8, PT1_ITEMS = 8;")],
+    "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
+    "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }
 CAPI_PATCHES = {
     "front": [('    if (tm) tm->mark("edge_pass");\n    HIP_CHECK(hipEventSynchronize(c.bins_ev));',

@@ -1494,7 +1494,9 @@ void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* r
                      unsigned long long* cursor, const unsigned long long* cap_end, uint64_t* out,
                      uint32_t* ovf, hipStream_t s) {
   if (m == 0) return;
-  constexpr int NT = 512, IT = 16;  // 8192-record tiles, 64 KB stage: two blocks per CU
+  // 8192-record tiles, 64 KB stage: two blocks of 16 waves per CU (RMAT-26 edge phase: 512 x
+  // 16 -> 8.9 ms, 1024 x 16 -> 10.8, 512 x 8 -> 8.5, 1024 x 8 -> 7.8)
+  constexpr int NT = 1024, IT = 8;
   const unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
   auto k = pre ? k_edge_bin<true, NT, IT> : k_edge_bin<false, NT, IT>;
   hipLaunchKernelGGL(k, dim3(nt), dim3(NT), 0, s, (const uint2*)uv, m, rank, n_rank, err, bins, nb,
@@ -1520,6 +1522,7 @@ static constexpr int PT_ITEMS = 16;
 // the degree kernels it overlaps); the second runs alone and uses 512 (8192 records, 64 KB:
 // two blocks per CU, so one streams while the other is between barriers; RMAT-26 7.7 -> 6.3 ms).
 static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;
+static constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;
 
 
 // Global histogram of the y digits (the first partition's run sizes).
@@ -1551,11 +1554,12 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
   hist[t] = 0;
 }
 
-template <int MODE, int NT>
+template <int MODE, int NT, int IT>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh,
        const uint32_t* __restrict__ rank, uint32_t n_rank) {
+  constexpr int PT_ITEMS = IT;
   constexpr int TILE = NT * PT_ITEMS;
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[256], tstart[256], hx[256], wsum[NT / 64];
@@ -1646,8 +1650,8 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
     hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
   }
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
-  uint64_t nt = (m + PT0_THREADS * PT_ITEMS - 1) / (PT0_THREADS * PT_ITEMS);
-  hipLaunchKernelGGL((k_part<0, PT0_THREADS>), dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m,
+  uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS>), dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m,
                      mid, cursor, xhist, sh, (const uint32_t*)nullptr, n_rank);
 }
 
@@ -1657,9 +1661,9 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   const int sh = part_shift(n_rank);
   uint32_t* xhist = ws + 256;
   unsigned long long* cursor = (unsigned long long*)(ws + 512);
-  uint64_t nt = (m + PT1_THREADS * PT_ITEMS - 1) / (PT1_THREADS * PT_ITEMS);
+  uint64_t nt = (m + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
   hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, xhist, cursor);
-  hipLaunchKernelGGL((k_part<1, PT1_THREADS>), dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, m,
+  hipLaunchKernelGGL((k_part<1, PT1_THREADS, PT1_ITEMS>), dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, m,
                      pre, cursor, xhist, sh, rank, n_rank);
 }
 
