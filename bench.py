@@ -208,13 +208,14 @@ def main():
         # bracketed live by HIP events on the stream they run on:
         #   k_kb_map (one launch per bucket, side stream): 8 B per record streamed + 4 B per
         #     rank of hi counts; its union-find / label gathers are not algorithmic bytes;
-        #   k_edge_pass (one launch): 8 B record read + 8 B item written + 2 x 4 B rank words.
+        #   k_edge_bin (one launch, the direct-binning edge pass over k_part's (x, rank y)
+        #     records): 8 B record read + 4 B rank word gathered + 8 B item written.
         avg = {k: sum(v) / len(v) for k, v in phase.items()}
         recs = hi - lo if world > 1 else m
         key = "rmat%d" % scale if args.workload == "rmat" else args.workload
         cands = []
         if "edge_pass" in avg:
-            cands.append(("k_edge_pass_tiles", avg["edge_pass"], 1, 24 * recs))
+            cands.append(("k_edge_bin", avg["edge_pass"], 1, 20 * recs))
         if avg.get("kb_map#"):
             cands.append(("k_kb_map", avg["kb_map"], avg["kb_map#"], 8 * recs + 4 * n_seq))
         roof = None

@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """Per-bucket kernel time (us) of the kb tree build from a rocprofv3 --kernel-trace csv:
-the last tree build in the trace (from its last k_kb_bounds launch)."""
+the last tree build in the trace (from the last launch that ends the grouping by hi:
+k_edge_bin, k_bin_scatter or k_kb_bounds)."""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_kb_bounds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows)
+       if any(k in r["Kernel_Name"] for k in ("k_kb_bounds", "k_edge_bin", "k_bin_scatter"))]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else -1
 last = rows[idx[which]:idx[which + 1]] if which != -1 else rows[idx[-1]:]
 per = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -22,6 +24,8 @@ for r in last:
         b += 1
     if "kb_" not in n:
         continue
+    if b < 0:
+        b = 0
     per[b][n] += d
     tot[n] += d
     t_end = max(t_end, int(r["End_Timestamp"]))
