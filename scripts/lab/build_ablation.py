@@ -134,6 +134,43 @@ PATCHES = {
     # (timing-only ablations that leave buffers unwritten are NOT safe: one of them hung and
     # faulted the GPU — garbage ids reach kernels that index with them.  Keep variants exact.)
     "front": [],
+    # map blocks of 256 / 512 threads keeping the 32K-rank window (fewer map waves per CU beside the apply)
+    "m256": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 256;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 2048; "),
+             ("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, 2 * device_cus());")],
+    "m512": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 512;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 4096; "),
+             ("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, 2 * device_cus());")],
+    "m512g1": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 512;"),
+             ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 4096; ")],
+    # degree kernels (correct results): loads in flight, flat write-out of the staged runs
+    "h16v2": [("  uint32_t acc[64];\n#pragma unroll\n  for (int k = 0; k < 64; ++k) acc[k] = 0;\n  constexpr int V = 4;",
+               "  uint32_t acc[64];\n#pragma unroll\n  for (int k = 0; k < 64; ++k) acc[k] = 0;\n  constexpr int V = 2;")],
+    "h16v8": [("  uint32_t acc[64];\n#pragma unroll\n  for (int k = 0; k < 64; ++k) acc[k] = 0;\n  constexpr int V = 4;",
+               "  uint32_t acc[64];\n#pragma unroll\n  for (int k = 0; k < 64; ++k) acc[k] = 0;\n  constexpr int V = 8;")],
+    "dsu4": [("  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;\n  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);\n  constexpr int U = 8;\n  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {\n    uint2 ee[U];",
+              "  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;\n  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);\n  constexpr int U = 4;\n  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {\n    uint2 ee[U];")],
+    "dsu16": [("  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;\n  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);\n  constexpr int U = 8;\n  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {\n    uint2 ee[U];",
+               "  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;\n  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);\n  constexpr int U = 16;\n  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {\n    uint2 ee[U];")],
+    "dsflat": [("""  // each wave writes whole bucket runs
+  for (uint32_t b = w; b < NB; b += DEGB_THREADS / 64) {
+    uint32_t s0 = start[b], n = cur[b] - s0;
+    uint64_t g = goff[b];
+    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];
+  }""", """  // flat write-out: thread t writes staged positions t, t + 1024, ...; the bucket of position
+  // p is found from the bucket of position 64 (p / 64) (segment table) and a short forward scan
+  __shared__ uint16_t segb[2 * DEGB_CHUNK / 64];
+  for (uint32_t b = t; b < NB; b += DEGB_THREADS) {
+    const uint32_t s0 = start[b], s1 = cur[b];
+    for (uint32_t q = (s0 + 63) / 64; q * 64 < s1; ++q) segb[q] = (uint16_t)b;
+  }
+  __syncthreads();
+  const uint32_t total = cur[NB - 1];
+  for (uint32_t p = t; p < total; p += DEGB_THREADS) {
+    uint32_t b = segb[p >> 6];
+    while (cur[b] <= p) ++b;
+    ep[goff[b] + (p - start[b])] = buf[p];
+  }""")],
     "p1k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
               "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 1024;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = 8;")],
     "p0k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
