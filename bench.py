@@ -233,7 +233,9 @@ def main():
                                       "GB_s": round(c[3] / (c[1] * 1e-3) / 1e9, 1),
                                       "traffic_per_launch": pmc_traffic(c[0], key)}
                                for c in cands if c[0] != name}}
-        path_bytes = 16 * m + 24 * n_seq  # SURVEY §8d B(m, n)
+        # SURVEY §8d B(m, n) = 16 m + 24 n with n = the id slots (its C4 row: 18.79 GB); the ids
+        # of degree 0 are never touched by the sequence or the tree, so 24 n_seq is given beside
+        path_bytes = 16 * m + 24 * n_ids
         label = "RMAT-%d" % scale if args.workload == "rmat" else wl["workload"]
         rec = {
             "metric": "edges/sec to build elimination tree (%s)" % label,
@@ -245,7 +247,8 @@ def main():
                            parallelism=("edge-shard x%d (%s)" % (world, args.dist)
                                         if world > 1 else "single")),
             "path_roofline": {"bytes": path_bytes,
-                              "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK)},
+                              "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK),
+                              "bytes_nseq": 16 * m + 24 * n_seq},
             "roofline": roof,
         }
         if args.check:

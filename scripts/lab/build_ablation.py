@@ -134,6 +134,8 @@ PATCHES = {
     # (timing-only ablations that leave buffers unwritten are NOT safe: one of them hung and
     # faulted the GPU — garbage ids reach kernels that index with them.  Keep variants exact.)
     "front": [],
+    # two map blocks per CU (for the unpipelined loop, where the map has the chip to itself)
+    "mg2": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, 2 * device_cus());")],
     # map blocks of 256 / 512 threads keeping the 32K-rank window (fewer map waves per CU beside the apply)
     "m256": [("static constexpr int KM_THREADS = 1024;", "static constexpr int KM_THREADS = 256;"),
              ("static constexpr int KM_CHUNK = 8192; ", "static constexpr int KM_CHUNK = 2048; "),

@@ -2061,7 +2061,8 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
   __shared__ uint32_t sbins[512];
-  __shared__ unsigned long long s_s0[512], s_s1[512];  // the bucket's segments [s0, s1)
+  __shared__ unsigned long long s_s0[512];  // the bucket's segments [s0, s0 + len)
+  __shared__ uint32_t s_len[512];
   __shared__ uint32_t s_cp[513];                        // chunks before each segment
   constexpr int R = KM_R;
   // RG: the giant's union-find root, found from the anchor rank (see launch_kb_map); it does
@@ -2091,18 +2092,18 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     nseg = sg.i1 - sg.i0;
     for (uint32_t i = t; i < nseg; i += KM_THREADS) {
       s_s0[i] = sg.start[sg.i0 + i];
-      s_s1[i] = min(sg.cur[sg.i0 + i], sg.cap[sg.i0 + i]);
+      s_len[i] = (uint32_t)(min(sg.cur[sg.i0 + i], sg.cap[sg.i0 + i]) - s_s0[i]);
     }
   } else if (t == 0) {
     s_s0[0] = e_begin;
-    s_s1[0] = e_end;
+    s_len[0] = (uint32_t)(e_end - e_begin);
   }
   __syncthreads();
   if (w == 0) {
     uint32_t run = 0;
     for (uint32_t b0 = 0; b0 < nseg; b0 += 64) {
       const uint32_t i = b0 + lane;
-      const uint32_t c = i < nseg ? (uint32_t)((s_s1[i] - s_s0[i] + KM_CHUNK - 1) / KM_CHUNK) : 0u;
+      const uint32_t c = i < nseg ? (uint32_t)(((uint64_t)s_len[i] + KM_CHUNK - 1) / KM_CHUNK) : 0u;
       const uint32_t incl = wave_incl_scan(c);
       if (i < nseg) s_cp[i] = run + incl - c;
       run += (uint32_t)__shfl((int)incl, 63);
@@ -2132,7 +2133,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
   auto fetch = [&](uint32_t j) {
     while (s_cp[si + 1] <= j) ++si;
     nc0 = s_s0[si] + (uint64_t)(j - s_cp[si]) * KM_CHUNK;
-    nc1 = min(nc0 + (uint64_t)KM_CHUNK, s_s1[si]);
+    nc1 = min(nc0 + (uint64_t)KM_CHUNK, s_s0[si] + s_len[si]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const uint64_t idx = nc0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
