@@ -47,6 +47,7 @@ static const KnobDef kKnobs[] = {
     {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
+    {"kb_pick", &Knobs::kb_pick},
 };
 
 static Knobs g_knobs;
@@ -395,6 +396,9 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // giant bitmap (k_kb_map) and the two slots of its reference vertex (INV: none yet)
   uint32_t* gbits = (uint32_t*)c.scratch.get("kb_gbits", bm_words * 4);
   uint32_t* gx = (uint32_t*)c.scratch.get("kb_gx", 2 * 4);
+  // the giant's anchor of each map, picked on the device (two slots by bucket parity)
+  uint32_t* anc = knobs().kb_pick ? (uint32_t*)c.scratch.get("kb_anchor", 2 * 4) : nullptr;
+  if (anc) (void)hipMemsetAsync(anc, 0xFF, 2 * 4, s);
   (void)hipMemsetAsync(counters, 0, 2 * 64, s);
   (void)hipMemsetAsync(bitmaps, 0, 2 * bm_words * 4, s);
   (void)hipMemsetAsync(gx, 0xFF, 2 * 4, s);
@@ -455,6 +459,12 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   const bool defer = knobs().kb_defer != 0;
   hipStream_t sa = s;  // the applies and the rebases between them
   auto rebase = [&](size_t j) {
+    if (anc) {  // the anchor of map j, then the bitmap's rebase on it
+      const uint32_t a = anchor_of(j);
+      launch_kb_pick(uf, a == INV ? 0u : a + 1, anc + ((j - 1) & 1), anc + (j & 1), gbits, n_seq,
+                     gx + ((j - 1) & 1), gx + (j & 1), sa);
+      return;
+    }
     if (!gbits) return;
     launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), sa);
   };
@@ -471,7 +481,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
                   seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
                   anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
                   lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer,
-                  st, seg ? &sg : nullptr);
+                  st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr);
     if (tm) tm->span_end(sp, st);
   };
   auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
@@ -479,7 +489,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     launch_kb_apply(recs(k) > 0, bk[k].first, bk[k + 1].first, anchor_of(k),
                     uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
                     spqs + p * spq_words, counters + p * 16, defer || (pipe && knobs().kb_refresh), stats,
-                    ws, gbits, gbits ? gx + (slot & 1) : nullptr, st);
+                    ws, gbits, gbits ? gx + (slot & 1) : nullptr, st, anc ? anc + (k & 1) : nullptr,
+                    anc ? anc + ((k + 1) & 1) : nullptr);
   };
   if (pipe) {
     // map k+1 runs on the side stream while bucket k is applied; the rebase for map k+1 sits

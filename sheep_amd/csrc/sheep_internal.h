@@ -52,6 +52,7 @@ struct Knobs {
   int tree_stats = 0;    // SHEEP_TREE_STATS: 1 totals, 2 per bucket (stderr; diagnostics)
   int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
   int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
+  int kb_pick = 1;       // SHEEP_KB_PICK: the giant's anchor picked on the device (0: rank B0 - 1)
 };
 Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
 
@@ -193,7 +194,14 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,
                    const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
                    bool defer /* misses kept as (b, a) for launch_kb_apply's refresh */,
-                   hipStream_t s, const KbSegs* segs = nullptr);
+                   hipStream_t s, const KbSegs* segs = nullptr,
+                   const uint32_t* anc = nullptr /* device-picked anchor (launch_kb_pick) */);
+// The giant's anchor for the next map, picked on the device among ranks [0, B0lim) (the
+// component holding most of an even sample; see sheep_kernels.hip), written to *anc_out (INV
+// when B0lim = 0); gbits (nullable): the bitmap is then rebased on it (launch_gb_rebase).
+void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,
+                    uint32_t* gbits, uint32_t n_seq, const uint32_t* gx_rd, uint32_t* gx_wr,
+                    hipStream_t s);
 // Before a map (nothing else touching the union-find): keep the giant bitmap's reference
 // vertex (*gx_rd) if it is in the anchor's component, else move it to the anchor and clear
 // the bitmap (n_seq / 32 + 2 words); the result goes to *gx_wr.
@@ -205,7 +213,9 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
                      bool refresh, bool stats, unsigned long long* st, uint32_t* gbits,
-                     const uint32_t* gx, hipStream_t s);
+                     const uint32_t* gx, hipStream_t s,
+                     const uint32_t* anc = nullptr /* this bucket's device anchor */,
+                     const uint32_t* anc_next = nullptr /* the next map's: its root is kept */);
 // Lockstep exchange of one bucket (sheep_ls_*): pack this rank's mark words [w0, w1] (ms u64
 // slots) and kept pairs (padded to cap) for an all-gather; unpack P such blocks into the
 // bitmap (OR) and a contiguous kept array, setting *n_kept = P * cap.

@@ -2044,6 +2044,12 @@ __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, u
 // chunk's first group go to LDS (bitmap + packed 16-bit counts) and reach global memory once
 // per word per chunk — a hub's records span many waves, and same-word atomics from every
 // wave serialise.  Ranks beyond the window use global atomics directly.
+// The anchor a kernel works with: the device-picked one (anc, k_kb_pick) when the host says
+// there is one, else the host's.
+__device__ __forceinline__ uint32_t anchor_rank(uint32_t anchor, const uint32_t* anc) {
+  return (anc && anchor != INV) ? *anc : anchor;
+}
+
 static constexpr int KM_THREADS = 1024;
 static constexpr int KM_CHUNK = 8192;       // < 65536: the packed 16-bit counts cannot carry
 static constexpr uint32_t KM_WIN = 32768;   // ranks
@@ -2056,7 +2062,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
          uint32_t B0, int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
-         const uint32_t* __restrict__ gx, int defer) {
+         const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc) {
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -2069,6 +2075,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
   // not move while this map runs (k_kb_union links everything else below it).  Membership is
   // tested on the root, not on the label, which the apply of the previous bucket may be
   // rewriting meanwhile.
+  anchor = anchor_rank(anchor, anc);
   const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   const bool use_bm = gbits != nullptr && RG != INV && *gx != INV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -2300,6 +2307,57 @@ __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf
       gbits[i] = 0;
 }
 
+// The giant's anchor, picked on the device before the map of a bucket, with nothing else
+// running on the union-find.  The host's choice, rank B0lim - 1 (the highest degree among the
+// applied ranks [0, B0lim)), can sit outside the giant: its bucket then sees no giant records
+// and the zipper walks the giant's spine unaided (twitter shape, 40 + 40 cuts: tree 31.6 ->
+// 47.8 ms).  So the first wave of every block samples 64 ranks spread evenly over [0, B0lim)
+// (the 64th is B0lim - 1) and finds the component holding the most samples; all blocks
+// compute the same answer.  The anchor is then
+//   the previous anchor, if its component still holds >= 4 samples and at least as many as
+//     the best one minus 2 (a move clears the giant bitmap);
+//   else a sampled rank of the best component, if it holds >= 4 samples (the giant: about
+//     6 % of the ranks or more);
+//   else B0lim - 1 (no dominant component yet: the host's choice).
+// Any applied rank is exact as an anchor (see launch_kb_map); the choice only shapes the work.
+// B0lim = 0: no anchor (INV).  gbits (nullable): the bitmap is then rebased on the anchor as
+// k_gb_rebase does.
+__global__ void __launch_bounds__(BLOCK)
+k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_prev,
+          uint32_t* anc_out, uint32_t* gbits, uint32_t nwords, const uint32_t* __restrict__ gx_rd,
+          uint32_t* gx_wr) {
+  __shared__ uint32_t s_anchor;
+  const int t = threadIdx.x, lane = t & 63;
+  if (t < 64) {
+    uint32_t anchor = INV;
+    if (B0lim > 0) {
+      const uint32_t smp = lane == 63 ? B0lim - 1 : (uint32_t)(((uint64_t)lane * B0lim) / 64);
+      const uint32_t r = uf_find_ro(uf, smp);
+      const uint32_t prev = *anc_prev;
+      const uint32_t rp = (prev != INV && prev < B0lim) ? uf_find_ro(uf, prev) : INV;
+      uint32_t cnt = 0;  // samples in this lane's component
+      for (int u = 0; u < 64; ++u) cnt += (uint32_t)__builtin_amdgcn_readlane((int)r, u) == r;
+      const uint32_t cp = (uint32_t)__popcll(__ballot(r == rp));
+      uint32_t key = (cnt << 8) | (uint32_t)lane;  // most samples, then the highest lane
+      for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o));
+      const uint32_t bc = key >> 8, bl = key & 0xFFu;
+      const uint32_t bs = bl == 63 ? B0lim - 1 : (uint32_t)(((uint64_t)bl * B0lim) / 64);
+      anchor = (rp != INV && cp >= 4 && cp + 2 >= bc) ? prev : (bc >= 4 ? bs : B0lim - 1);
+    }
+    if (t == 0) s_anchor = anchor;
+  }
+  __syncthreads();
+  const uint32_t anchor = s_anchor;
+  if (blockIdx.x == 0 && t == 0) *anc_out = anchor;
+  if (!gbits) return;
+  const uint32_t X = *gx_rd;
+  const bool keep = anchor == INV || (X != INV && uf_find_ro(uf, X) == uf_find_ro(uf, anchor));
+  if (blockIdx.x == 0 && t == 0) *gx_wr = anchor == INV ? INV : (keep ? X : anchor);
+  if (!keep)
+    for (uint32_t i = blockIdx.x * blockDim.x + t; i < nwords; i += gridDim.x * blockDim.x)
+      gbits[i] = 0;
+}
+
 // Star -> path for the giant.  G's edges into the bucket go to the marked ranks b1 < b2 < ...;
 // for the etree that star is equivalent to the path G-b1-b2-...: at every threshold both
 // connect G with exactly the marked ranks present.  The path edges (b_i, b_i+1) are written
@@ -2320,9 +2378,9 @@ __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf
 __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
                            uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit,
                            uint32_t* uf, uint32_t anchor, uint32_t* gbits,
-                           const uint32_t* __restrict__ gx) {
+                           const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc) {
   const uint32_t w0 = B0 >> 5, w1 = (B1 - 1) >> 5;
-  const uint32_t R = uf_find_ro(uf, anchor);
+  const uint32_t R = uf_find_ro(uf, anchor_rank(anchor, anc));
   const uint32_t X = gbits ? *gx : INV;
   const bool set_g = X != INV && uf_find_ro(uf, X) == R;
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
@@ -2366,8 +2424,9 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept,
                              uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* bitmap,
                              uint32_t B0, uint32_t anchor, uint32_t* gbits,
-                             const uint32_t* __restrict__ gx) {
+                             const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc) {
   const uint32_t nk = *n_kept;
+  anchor = anchor_rank(anchor, anc);
   const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   const uint32_t X = gbits ? *gx : INV;
   const bool set_g = X != INV && RG != INV && uf_find_ro(uf, X) == RG;
@@ -2400,7 +2459,7 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
                          uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
                          uint32_t* jump, unsigned long long* stats, uint32_t* linked,
                          uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
-                         uint32_t qchunk) {
+                         uint32_t qchunk, const uint32_t* __restrict__ anc) {
   constexpr uint32_t LCAP = 2048;
   __shared__ uint32_t lbuf[LCAP];
   __shared__ uint32_t lcnt, lbase;
@@ -2415,6 +2474,7 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   rec.lcap = LCAP;
   EdgeSrc src{kept};
   const uint64_t nk = *n_kept;
+  anchor = anchor_rank(anchor, anc);
   if (anchor != INV) {
     SpineInfo sp;
     sp.bitmap = bitmap;
@@ -2447,7 +2507,8 @@ template <bool FOLD>
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
                            uint32_t B1, const uint32_t* __restrict__ linked,
                            const uint32_t* __restrict__ n_linked, uint32_t* bitmap,
-                           uint32_t anchor) {
+                           uint32_t anchor, const uint32_t* __restrict__ anc) {
+  anchor = anchor_rank(anchor, anc);
   const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
   // with the next bucket hold no marks of it yet; the previous bucket cleared its own)
@@ -2562,7 +2623,8 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
-                   const uint32_t* gx, bool defer, hipStream_t s, const KbSegs* segs) {
+                   const uint32_t* gx, bool defer, hipStream_t s, const KbSegs* segs,
+                   const uint32_t* anc) {
   // segs: e_begin / e_end bound the bucket's records (the capacity of its bins)
   if (e_end <= e_begin) return;
   KbSegs sg{};
@@ -2578,7 +2640,16 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, sg, B0, gshift,
                      uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx, (int)defer);
+                     gx ? gbits : nullptr, gx, (int)defer, anc);
+}
+
+void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,
+                    uint32_t* gbits, uint32_t n_seq, const uint32_t* gx_rd, uint32_t* gx_wr,
+                    hipStream_t s) {
+  const uint32_t nwords = n_seq / 32 + 2;
+  const unsigned grid = gbits ? std::min<uint32_t>((nwords + BLOCK - 1) / BLOCK, 1024) : 1u;
+  hipLaunchKernelGGL(k_kb_pick, dim3(grid), dim3(BLOCK), 0, s, uf, B0lim, anc_prev, anc_out, gbits,
+                     nwords, gx_rd, gx_wr);
 }
 
 void launch_gb_rebase(uint32_t* gbits, uint32_t n_seq, const uint32_t* uf, uint32_t anchor,
@@ -2592,7 +2663,8 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
                      bool refresh, bool stats, unsigned long long* st, uint32_t* gbits,
-                     const uint32_t* gx, hipStream_t s) {
+                     const uint32_t* gx, hipStream_t s, const uint32_t* anc,
+                     const uint32_t* anc_next) {
   const uint32_t scan_limit = 64;  // spine scan: bitmap words per search
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
@@ -2601,11 +2673,11 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   if (nonempty) {
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
-                         uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx);
+                         uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc);
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
-                         uf, anchor, gbits, gx);
+                         uf, anchor, gbits, gx, anc);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
     // zipper queue: edges per wave refill (tree phase, RMAT-26: 26.3 / 25.6 / 25.3 / 25.8 ms at
     // 64 / 256 / 512 / 1024; twitter-shape: 37.7 / 37.6 / 38.9 ms at 64 / 256 / 512; LJ-shape
@@ -2614,7 +2686,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
-                       anchor, scan_limit, qchunk);
+                       anchor, scan_limit, qchunk, anc);
   }
   // giant fold: the marks are relative to the anchor's component; its root R_a may later be
   // linked below the union's R (pipelined: different anchors) — the folded ranks follow it
@@ -2625,7 +2697,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
   hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,
-                     B0 > 0 ? B0 - 1 : INV);
+                     B0 > 0 ? B0 - 1 : INV, anc_next);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for((uint64_t)(B1 - B0) + 64)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold,
                      gbits, gx);
