@@ -359,12 +359,12 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 
 // kb bucket counts: each bucket costs a fixed ~60-100 us of launches and small kernels, while
 // too few buckets leave the zipper long in-bucket walks (profiles/r01/kb_bucket_sweep.txt).
-// kmax: 48 for the one-GPU loop (RMAT-26, K_e = K_r = 32/40/48/64/80 -> 81.6/71.9/71.9/74.4/
-// 76.1 ms, profiles/r01/kb_bucket_sweep_r01b.txt: below ~40 a bucket's in-bucket walks grow
-// long, above it the fixed per-bucket cost dominates); 40 for the lockstep loop, whose
-// critical path is the apply (RMAT-26, P = 8 simulation: K = 40/48/56/64 -> apply
-// 18.8/18.7/19.2/20.5 ms).
-static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 48) {
+// kmax = 40 (below ~40 a bucket's in-bucket walks grow long, above it the fixed per-bucket
+// cost dominates).  With the device-picked anchor (launch_kb_pick), tree phase at K_e = K_r =
+// 32/36/40/44/48: RMAT-26 25.5/20.4/19.8/22.5/20.6 ms, twitter shape (32/40/48) 29.1/29.6/30.4
+// ms, RMAT-25 (40/48) 12.3/13.8 ms (profiles/r02/lab/lab_kpick.jsonl); the lockstep loop's
+// apply at P = 8, K = 40/48/56/64: 18.8/18.7/19.2/20.5 ms (round 1).
+static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 40) {
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
   *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : K_auto;
   *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
@@ -607,7 +607,7 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 // The cuts as bin indices (sorted, distinct, in (0, nb - 1)).
 static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                                          const std::vector<unsigned long long>& bin_start,
-                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 48) {
+                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 40) {
   const uint32_t nb = (uint32_t)bounds.size();
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;

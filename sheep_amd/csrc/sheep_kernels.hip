@@ -2311,43 +2311,53 @@ __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf
 // running on the union-find.  The host's choice, rank B0lim - 1 (the highest degree among the
 // applied ranks [0, B0lim)), can sit outside the giant: its bucket then sees no giant records
 // and the zipper walks the giant's spine unaided (twitter shape, 40 + 40 cuts: tree 31.6 ->
-// 47.8 ms).  So the first wave of every block samples 64 ranks spread evenly over [0, B0lim)
-// (the 64th is B0lim - 1) and finds the component holding the most samples; all blocks
-// compute the same answer.  The anchor is then
-//   the previous anchor, if its component still holds >= 4 samples and at least as many as
-//     the best one minus 2 (a move clears the giant bitmap);
-//   else a sampled rank of the best component, if it holds >= 4 samples (the giant: about
-//     6 % of the ranks or more);
+// 47.8 ms).  So every block samples KP ranks spread evenly over [0, B0lim) (the last one is
+// B0lim - 1) and finds the component holding the most samples; all blocks compute the same
+// answer.  Two evenly spaced samples land in one component only if it spans about 1/KP of the
+// ranks: beyond a couple of samples that is the giant.  The anchor is then
+//   the previous anchor, if its component still holds >= 3 samples and at least the best
+//     count minus 4 (a move clears the giant bitmap);
+//   else a sampled rank of the best component, if it holds >= 3 samples;
 //   else B0lim - 1 (no dominant component yet: the host's choice).
 // Any applied rank is exact as an anchor (see launch_kb_map); the choice only shapes the work.
 // B0lim = 0: no anchor (INV).  gbits (nullable): the bitmap is then rebased on the anchor as
 // k_gb_rebase does.
+static constexpr int KP = BLOCK;  // samples (one per thread of a block)
 __global__ void __launch_bounds__(BLOCK)
 k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_prev,
           uint32_t* anc_out, uint32_t* gbits, uint32_t nwords, const uint32_t* __restrict__ gx_rd,
           uint32_t* gx_wr) {
+  __shared__ uint32_t roots[KP], wkey[KP / 64], wcp[KP / 64];
   __shared__ uint32_t s_anchor;
-  const int t = threadIdx.x, lane = t & 63;
-  if (t < 64) {
-    uint32_t anchor = INV;
-    if (B0lim > 0) {
-      const uint32_t smp = lane == 63 ? B0lim - 1 : (uint32_t)(((uint64_t)lane * B0lim) / 64);
-      const uint32_t r = uf_find_ro(uf, smp);
-      const uint32_t prev = *anc_prev;
-      const uint32_t rp = (prev != INV && prev < B0lim) ? uf_find_ro(uf, prev) : INV;
-      uint32_t cnt = 0;  // samples in this lane's component
-      for (int u = 0; u < 64; ++u) cnt += (uint32_t)__builtin_amdgcn_readlane((int)r, u) == r;
-      const uint32_t cp = (uint32_t)__popcll(__ballot(r == rp));
-      uint32_t key = (cnt << 8) | (uint32_t)lane;  // most samples, then the highest lane
-      for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o));
-      const uint32_t bc = key >> 8, bl = key & 0xFFu;
-      const uint32_t bs = bl == 63 ? B0lim - 1 : (uint32_t)(((uint64_t)bl * B0lim) / 64);
-      anchor = (rp != INV && cp >= 4 && cp + 2 >= bc) ? prev : (bc >= 4 ? bs : B0lim - 1);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t anchor = INV;
+  if (B0lim > 0) {  // uniform over the block
+    const uint32_t smp = t == KP - 1 ? B0lim - 1 : (uint32_t)(((uint64_t)t * B0lim) / KP);
+    const uint32_t r = uf_find_ro(uf, smp);
+    roots[t] = r;
+    const uint32_t prev = *anc_prev;
+    const uint32_t rp = (prev != INV && prev < B0lim) ? uf_find_ro(uf, prev) : INV;
+    __syncthreads();
+    uint32_t cnt = 0;  // samples in this thread's component
+    for (int u = 0; u < KP; ++u) cnt += roots[u] == r;
+    uint32_t key = (cnt << 16) | (uint32_t)t;  // most samples, then the highest thread
+    uint32_t cp = r == rp ? cnt : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+      key = max(key, (uint32_t)__shfl_xor((int)key, o));
+      cp = max(cp, (uint32_t)__shfl_xor((int)cp, o));
     }
-    if (t == 0) s_anchor = anchor;
+    if (lane == 0) { wkey[w] = key; wcp[w] = cp; }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t bk = 0, bp = 0;
+      for (int i = 0; i < KP / 64; ++i) { bk = max(bk, wkey[i]); bp = max(bp, wcp[i]); }
+      const uint32_t bc = bk >> 16, bt = bk & 0xFFFFu;
+      const uint32_t bs = bt == KP - 1 ? B0lim - 1 : (uint32_t)(((uint64_t)bt * B0lim) / KP);
+      s_anchor = (rp != INV && bp >= 3 && bp + 4 >= bc) ? prev : (bc >= 3 ? bs : B0lim - 1);
+    }
+    __syncthreads();
+    anchor = s_anchor;
   }
-  __syncthreads();
-  const uint32_t anchor = s_anchor;
   if (blockIdx.x == 0 && t == 0) *anc_out = anchor;
   if (!gbits) return;
   const uint32_t X = *gx_rd;

@@ -325,6 +325,8 @@ KB_KNOBS = [
     {"kb_refresh": 0},                               # pipelined, stale kept starts zipped as they are
     {"sort": 1},                                     # two 9-bit radix passes instead of hi bins
     {"kb_pipe": 1, "kb_buckets": 512, "kb_rankb": 512},  # many narrow buckets
+    {"kb_pick": 0},                                  # the host's anchor (rank B0 - 1) for every map
+    {"kb_pick": 0, "kb_pipe": 0},
 ]
 
 
