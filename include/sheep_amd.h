@@ -174,6 +174,9 @@ int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_
  *                    them: cap may exceed this shard's m);
  *                    [all-gather of d_send[0, S + cap) from every rank into d_recv];
  *                    sheep_ls_apply(k, d_recv, P, cap).
+ *                    Order: sheep_ls_map(k + 1) is called after sheep_ls_apply(k) has been
+ *                    called (it may run while that apply runs): the apply of bucket k picks
+ *                    the giant's anchor of map k + 1 on the device, and the map waits for it.
  *   sheep_ls_finish  d_parent (n_seq, identical on every rank) and d_pst (n_seq) of THIS
  *                    shard's records from its own degrees d_deg / d_selfc (sum over ranks =
  *                    the tree's pst_weight).  Synchronises.

@@ -864,7 +864,13 @@ struct Lockstep {
   uint32_t* h_pinned = nullptr;
   size_t kept_bytes = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, apply_ev;
+  // the giant's anchor of each map, picked on the device by the apply of the bucket before
+  // (launch_kb_pick; identical on every rank: the replicas are identical), two slots by parity
+  uint32_t* anc = nullptr;
+  hipEvent_t pick_ev[2] = {nullptr, nullptr};
   ~Lockstep() {
+    for (auto& e : pick_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto& e : map_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     for (auto& e : apply_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (h_pinned) (void)hipHostFree(h_pinned);
@@ -912,6 +918,11 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   L.bitmap = (uint32_t*)sc.get("ls_bitmap", 2 * bm_words * 4);
   L.spq = (uint32_t*)sc.get("ls_spq", 2 * spq_words * 4);
   L.ws = (unsigned long long*)sc.get("ls_ws", 128);
+  if (knobs().kb_pick) {
+    L.anc = (uint32_t*)sc.get("ls_anchor", 2 * 4);
+    HIP_CHECK(hipMemsetAsync(L.anc, 0xFF, 2 * 4, s));
+    for (auto& e : L.pick_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   launch_fill(L.parent, INV, n, s);
   launch_fill(L.jump, 0, n, s);
   launch_fill(L.hcnt, 0, n, s);
@@ -1003,10 +1014,13 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
                    uint32_t* n_kept_out, hipStream_t s) {
   if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
   const uint32_t B0 = L.bk[k].first;
+  // the anchor of this map was picked by the apply of bucket k-1 (on the apply's stream)
+  if (L.anc && k >= 1) HIP_CHECK(hipStreamWaitEvent(s, L.pick_ev[k & 1], 0));
   auto ev = L.span(L.map_ev, s);
   launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
                 d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws, L.bins,
-                (uint32_t)L.bounds.size(), nullptr, nullptr, false, s);
+                (uint32_t)L.bounds.size(), nullptr, nullptr, false, s, nullptr,
+                L.anc ? L.anc + (k & 1) : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
@@ -1043,11 +1057,20 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
   }
   uint64_t* kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
+  // the anchor of map k+1 first: the union-find is as bucket k-1 left it (the caller applies
+  // in order on one stream and has waited for map k), and map k+1 waits for this pick
+  if (L.anc && k + 1 < L.global_e.size()) {
+    const uint32_t a = L.anchor(k + 1);
+    launch_kb_pick(L.uf, a == INV ? 0u : a + 1, L.anc + (k & 1), L.anc + ((k + 1) & 1), nullptr,
+                   L.n_seq, nullptr, nullptr, s);
+    HIP_CHECK(hipEventRecord(L.pick_ev[(k + 1) & 1], s));
+  }
   auto ev = L.span(L.apply_ev, s);
   launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
                   L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, nullptr,
-                  nullptr, s);
+                  nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
+                  L.anc ? L.anc + ((k + 1) & 1) : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
 }
 
