@@ -868,6 +868,11 @@ struct Lockstep {
   // (launch_kb_pick; identical on every rank: the replicas are identical), two slots by parity
   uint32_t* anc = nullptr;
   hipEvent_t pick_ev[2] = {nullptr, nullptr};
+  // direct binning (launch_edge_bin): the buckets' .second are bin indices and bin i's items
+  // lie at [cstart[i], fill); dseg: start | cursor | capacity end, 512 u64 each
+  bool direct = false;
+  std::vector<unsigned long long> cstart;
+  unsigned long long* dseg = nullptr;
   ~Lockstep() {
     for (auto& e : pick_ev)
       if (e) (void)hipEventDestroy(e);
@@ -895,10 +900,12 @@ struct Lockstep {
   }
 };
 
+// part_done (nullable): the first partition pass of the rank gathers was launched by the caller
+// into "ls_items" (with "part_ws" holding its cursors) and completes at this event.
 static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
-                     uint32_t* d_err, hipStream_t s) {
+                     uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr) {
   require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
@@ -946,7 +953,8 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   std::vector<uint64_t> hd(nch);
   HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  L.bounds = make_bins(hd, n_seq);
+  std::vector<double> est;
+  L.bounds = make_bins(hd, n_seq, &est);
   const uint32_t nb = (uint32_t)L.bounds.size();
   L.bins = (uint32_t*)sc.get("ls_bins", 512 * 4);
   HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
@@ -957,11 +965,53 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   uint32_t* tmp = (uint32_t*)sc.get("ls_rsort_tmp", rsort_tmp_words(mm) * 4);
   uint16_t* digits = (uint16_t*)sc.get("ls_item_bins", mm * 2);
   const uint32_t* src = d_uv;
-  const bool part = m >= (1ull << 22);
+  const bool part = use_part(m);
   if (part) {
-    uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", 1024 * 4);
-    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
+    if (part_done) {  // pass 1 ran beside the degree all-reduce and the sequence
+      uint32_t* pws = (uint32_t*)sc.get("part_ws", 1024 * 4);
+      HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
+    } else {
+      uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", 1024 * 4);
+      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
+    }
     src = (const uint32_t*)items_b;
+  }
+  // Direct binning, as the one-GPU path: this shard's share of each bin's estimate (the bins
+  // and estimates are global) sizes its capacity; a bin that outgrows it sends this rank
+  // through the scatter below (ranks may differ in that: only per-bin counts are exchanged).
+  if (knobs().bin_direct && m > 0) {
+    double W = 0;
+    for (double e : est) W += e;
+    const double share = W > 0 ? std::min(1.0, (double)m / W) : 1.0;
+    const double slack = 1.0 + knobs().bin_slack / 1000.0;
+    L.cstart.assign(nb, 0ull);
+    std::vector<unsigned long long> h(3 * 512, 0ull);
+    for (uint32_t i = 0; i + 1 < nb; ++i) {
+      const uint64_t cap = (uint64_t)std::ceil(est[i] * share * slack) + 8192;
+      L.cstart[i + 1] = L.cstart[i] + cap;
+      h[i] = h[512 + i] = L.cstart[i];
+      h[1024 + i] = L.cstart[i + 1];
+    }
+    L.dseg = (unsigned long long*)sc.get("ls_bin_segs", h.size() * 8);
+    HIP_CHECK(hipMemcpyAsync(L.dseg, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+    uint32_t* ovf = (uint32_t*)sc.get("ls_ovf", 4);
+    HIP_CHECK(hipMemsetAsync(ovf, 0, 4, s));
+    uint64_t* binned = (uint64_t*)sc.get("ls_binned", std::max<uint64_t>(L.cstart[nb - 1], 1) * 8);
+    launch_edge_bin(src, part, m, d_rank, n_rank, d_err, L.bins, nb, L.dseg + 512, L.dseg + 1024,
+                    binned, ovf, s);
+    std::vector<unsigned long long> cur(nb);
+    HIP_CHECK(hipMemcpyAsync(cur.data(), L.dseg + 512, nb * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(L.h_pinned, ovf, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (L.h_pinned[0] == 0) {
+      L.direct = true;
+      L.sorted = binned;
+      for (uint32_t i = 0; i + 1 < nb; ++i) counts_out[i] = cur[i] - L.cstart[i];
+      counts_out[nb - 1] = 0;  // INVALID his are not stored (no bucket reads them)
+      *nb_out = nb;
+      return;
+    }
   }
   unsigned long long* dstart = (unsigned long long*)sc.get("ls_bin_start", 513 * 8);
   L.sorted = group_by_bins(src, part, m, d_rank, n_rank, d_err, L.bins, nb, items, items_b, tmp,
@@ -997,7 +1047,7 @@ static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_ou
   bi.push_back(nb - 1);
   for (size_t k = 0; k < bi.size(); ++k) {
     const uint32_t r = k + 1 < bi.size() ? L.bounds[bi[k]] : L.n_seq;
-    L.bk.emplace_back(r, (uint64_t)L.local_start[bi[k]]);
+    L.bk.emplace_back(r, L.direct ? (uint64_t)bi[k] : (uint64_t)L.local_start[bi[k]]);
   }
   for (size_t k = 0; k + 1 < bi.size(); ++k) {
     L.global_e.push_back(gstart[bi[k + 1]] - gstart[bi[k]]);
@@ -1017,10 +1067,15 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   // the anchor of this map was picked by the apply of bucket k-1 (on the apply's stream)
   if (L.anc && k >= 1) HIP_CHECK(hipStreamWaitEvent(s, L.pick_ev[k & 1], 0));
   auto ev = L.span(L.map_ev, s);
-  launch_kb_map(L.sorted, L.bk[k].second, L.bk[k + 1].second, B0, L.anchor(k), L.uf, L.label,
-                d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws, L.bins,
-                (uint32_t)L.bounds.size(), nullptr, nullptr, false, s, nullptr,
-                L.anc ? L.anc + (k & 1) : nullptr);
+  KbSegs sg{};
+  if (L.direct)
+    sg = {L.dseg, L.dseg + 512, L.dseg + 1024, (uint32_t)L.bk[k].second,
+          (uint32_t)L.bk[k + 1].second};
+  launch_kb_map(L.sorted, L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second,
+                L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
+                L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
+                L.bins, (uint32_t)L.bounds.size(), nullptr, nullptr, false, s,
+                L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
@@ -1114,7 +1169,21 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   uint32_t* selfc = (uint32_t*)c.scratch.get("mt_selfc", n * 4);
   uint32_t* deg = (uint32_t*)c.scratch.get("mt_deg", n * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("mt_rank", n * 4);
-  degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s);
+  // the first partition pass of the rank gathers needs no ranks: it runs on the side stream
+  // beside the rest of the degree pass, the degree all-reduce and the sequence sort
+  const bool overlap = knobs().part_overlap != 0 && m > 0 && use_part(m);
+  hipEvent_t part_done = nullptr;
+  if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
+  const bool yh = degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s, overlap,
+                             overlap ? c.part_ev[0] : nullptr);
+  if (overlap) {
+    uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", m * 8);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
+    HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
+    part_done = c.part_ev[1];
+  }
   if (n_ids) HIP_CHECK(hipMemcpyAsync(deg, deg_local, (size_t)n_ids * 4, hipMemcpyDeviceToDevice, s));
   comm.allreduce_sum_u32(deg, n_ids, s);
   if (tm) tm->mark("degree");
@@ -1134,7 +1203,8 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   c.ls_live++;
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
-  ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s);
+  ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done);
+  if (part_done) HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));  // also when no tree is built
   check_err(c, s);
   uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);
   HIP_CHECK(hipMemcpyAsync(dcounts, counts.data(), (size_t)nb * 8, hipMemcpyHostToDevice, s));
