@@ -364,9 +364,12 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 // 32/36/40/44/48: RMAT-26 25.5/20.4/19.8/22.5/20.6 ms, twitter shape (32/40/48) 29.1/29.6/30.4
 // ms, RMAT-25 (40/48) 12.3/13.8 ms (profiles/r02/lab/lab_kpick.jsonl); the lockstep loop's
 // apply at P = 8, K = 40/48/56/64: 18.8/18.7/19.2/20.5 ms (round 1).
+// Edge-quantile cuts: 2/5 as many (at least 8): with the rank cuts at 40 and the device-picked
+// anchor, K_e = 8/12/16/24/32/40 -> RMAT-26 tree 19.2/19.0/18.9/19.1/19.4/19.7 ms, twitter shape
+// (12/16/24/40) 28.4/28.3/29.1/29.4 ms, RMAT-25 (16/40) 11.6/12.5 ms (lab_kcuts.jsonl).
 static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 40) {
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
-  *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : K_auto;
+  *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : std::max<uint32_t>(8, K_auto * 2 / 5);
   *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
 }
 
