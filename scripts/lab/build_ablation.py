@@ -134,6 +134,24 @@ PATCHES = {
     # (timing-only ablations that leave buffers unwritten are NOT safe: one of them hung and
     # faulted the GPU — garbage ids reach kernels that index with them.  Keep variants exact.)
     "front": [],
+    # streaming loads / stores of the edge-bin and partition passes non-temporal
+    "ebinnt": [("    e[k] = j < tile_n ? uv[tbase + j] : make_uint2(0, PRE ? RY_SELF : 0u);",
+                "    if (j < tile_n) { const uint64_t q = __builtin_nontemporal_load((const uint64_t*)uv + tbase + j); e[k] = make_uint2((uint32_t)q, (uint32_t)(q >> 32)); } else e[k] = make_uint2(0, PRE ? RY_SELF : 0u);")],
+    "ebonnt": [("""    const uint32_t s0 = tstart[d];
+    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];
+  }
+}
+
+void launch_edge_bin(""", """    const uint32_t s0 = tstart[d];
+    for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(stage[s0 + j], &out[g + j]);
+  }
+}
+
+void launch_edge_bin(""")],
+    "partnt": [("    rec[k] = j < tile_n ? in[tbase + j] : 0ull;", "    rec[k] = j < tile_n ? __builtin_nontemporal_load(&in[tbase + j]) : 0ull;"),
+               ("    out[gbase[d] + (j - tstart[d])] = r;", "    __builtin_nontemporal_store(r, &out[gbase[d] + (j - tstart[d])]);")],
+    # map record loads non-temporal (the streamed records should not evict the apply's working set)
+    "mapnt": [("      nx[r] = idx < nc1 ? items[idx] : 0ull;", "      nx[r] = idx < nc1 ? __builtin_nontemporal_load(&items[idx]) : 0ull;")],
     # two map blocks per CU (for the unpipelined loop, where the map has the chip to itself)
     "mg2": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, 2 * device_cus());")],
     # map blocks of 256 / 512 threads keeping the 32K-rank window (fewer map waves per CU beside the apply)

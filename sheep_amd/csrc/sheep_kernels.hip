@@ -2144,7 +2144,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const uint64_t idx = nc0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
-      nx[r] = idx < nc1 ? items[idx] : 0ull;
+      nx[r] = idx < nc1 ? __builtin_nontemporal_load(&items[idx]) : 0ull;  // streamed once
     }
     nh0 = (uint32_t)(items[nc0] >> 32);
     nbl = (uint32_t)(items[nc1 - 1] >> 32);
