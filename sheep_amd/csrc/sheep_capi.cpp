@@ -727,7 +727,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     plan.cstart.assign(nbins, 0ull);
     std::vector<unsigned long long> h(3 * 512, 0ull);  // start | cursor | capacity end
     for (uint32_t i = 0; i + 1 < nbins; ++i) {
-      const uint64_t cap = (uint64_t)std::ceil(est[i] * slack) + 8192;
+      // a bin never holds more than m items (and the map keeps segment lengths in u32)
+      const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(est[i] * slack) + 8192, m);
       plan.cstart[i + 1] = plan.cstart[i] + cap;
       h[i] = h[512 + i] = plan.cstart[i];
       h[1024 + i] = plan.cstart[i + 1];
@@ -991,7 +992,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     L.cstart.assign(nb, 0ull);
     std::vector<unsigned long long> h(3 * 512, 0ull);
     for (uint32_t i = 0; i + 1 < nb; ++i) {
-      const uint64_t cap = (uint64_t)std::ceil(est[i] * share * slack) + 8192;
+      const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(est[i] * share * slack) + 8192, m);
       L.cstart[i + 1] = L.cstart[i] + cap;
       h[i] = h[512 + i] = L.cstart[i];
       h[1024 + i] = L.cstart[i + 1];
