@@ -877,6 +877,10 @@ struct Lockstep {
   bool direct = false;
   std::vector<unsigned long long> cstart;
   unsigned long long* dseg = nullptr;
+  // giant bitmap of this rank's maps (set bits are exact, so ranks may differ in them: they
+  // only spare finds) and the two slots of its reference vertex; rebased by the pick
+  uint32_t* gbits = nullptr;
+  uint32_t* gx = nullptr;
   ~Lockstep() {
     for (auto& e : pick_ev)
       if (e) (void)hipEventDestroy(e);
@@ -933,6 +937,12 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     L.anc = (uint32_t*)sc.get("ls_anchor", 2 * 4);
     HIP_CHECK(hipMemsetAsync(L.anc, 0xFF, 2 * 4, s));
     for (auto& e : L.pick_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (knobs().kb_gbits) {
+      L.gbits = (uint32_t*)sc.get("ls_gbits", bm_words * 4);
+      L.gx = (uint32_t*)sc.get("ls_gx", 2 * 4);
+      HIP_CHECK(hipMemsetAsync(L.gbits, 0, bm_words * 4, s));
+      HIP_CHECK(hipMemsetAsync(L.gx, 0xFF, 2 * 4, s));
+    }
   }
   launch_fill(L.parent, INV, n, s);
   launch_fill(L.jump, 0, n, s);
@@ -1078,8 +1088,8 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   launch_kb_map(L.sorted, L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second,
                 L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
                 L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
-                L.bins, (uint32_t)L.bounds.size(), nullptr, nullptr, false, s,
-                L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr);
+                L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
+                false, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
@@ -1118,17 +1128,20 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   uint64_t* kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
   // the anchor of map k+1 first: the union-find is as bucket k-1 left it (the caller applies
   // in order on one stream and has waited for map k), and map k+1 waits for this pick
+  size_t gslot = k;  // the bitmap slot most recently written on this stream
   if (L.anc && k + 1 < L.global_e.size()) {
     const uint32_t a = L.anchor(k + 1);
-    launch_kb_pick(L.uf, a == INV ? 0u : a + 1, L.anc + (k & 1), L.anc + ((k + 1) & 1), nullptr,
-                   L.n_seq, nullptr, nullptr, s);
+    launch_kb_pick(L.uf, a == INV ? 0u : a + 1, L.anc + (k & 1), L.anc + ((k + 1) & 1), L.gbits,
+                   L.n_seq, L.gbits ? L.gx + (k & 1) : nullptr,
+                   L.gbits ? L.gx + ((k + 1) & 1) : nullptr, s);
     HIP_CHECK(hipEventRecord(L.pick_ev[(k + 1) & 1], s));
+    gslot = k + 1;
   }
   auto ev = L.span(L.apply_ev, s);
   launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
-                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, nullptr,
-                  nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
+                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, L.gbits,
+                  L.gbits ? L.gx + (gslot & 1) : nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
                   L.anc ? L.anc + ((k + 1) & 1) : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
 }

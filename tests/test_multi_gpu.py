@@ -85,3 +85,22 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
         assert np.array_equal(t.parent, p) and np.array_equal(t.pst, w)
     finally:
         device.comm_free()
+
+
+@pytest.mark.parametrize("env", [{"bin_slack": -900},               # every rank's bins overflow:
+                                                                    # the scatter path per rank
+                                 {"bin_direct": 0},                 # edge pass + bin scatter
+                                 {"kb_pick": 0},                    # the host's anchors
+                                 {"kb_gbits": 0},                   # no giant bitmap in the maps
+                                 {"part_overlap": 0}])              # no first pass beside the degrees
+def test_multi_local_front_half_options(oracle, gpu, options, env):
+    """The multi-rank driver under the front-half / anchor options: the same tree (R-MAT 19,
+    P = 2: 2^22 records per rank, so each rank runs the partitioned gathers)."""
+    import torch
+    from sheep_amd import device
+
+    options(**env)
+    uv_d = device.rmat(19, 16, 12)
+    torch.cuda.synchronize()
+    out = device.graph2tree_multi_local(shards_of(uv_d, 2), 1 << 19)
+    check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
