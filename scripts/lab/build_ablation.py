@@ -197,6 +197,13 @@ void launch_edge_bin(""")],
               "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = 8, PT1_ITEMS = PT_ITEMS;")],
     "p01k8": [("static constexpr int PT0_THREADS = 1024, PT1_THREADS = 512;\nstatic constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;",
                "static constexpr int PT0_THREADS = 1024, PT1_THREADS = 1024;\nstatic constexpr int PT0_ITEMS = 8, PT1_ITEMS = 8;")],
+    # second partition pass writing each tile's digit-sorted stage to the tile's own range
+    # (contiguous stores; the records stay exact, only their order changes) — with / without the
+    # cursor atomics: what the scattered runs and the reservations cost
+    "p1local": [("    out[gbase[d] + (j - tstart[d])] = r;", "    out[MODE == 1 ? tbase + j : gbase[d] + (j - tstart[d])] = r;")],
+    "p1noat": [("    out[gbase[d] + (j - tstart[d])] = r;", "    out[MODE == 1 ? tbase + j : gbase[d] + (j - tstart[d])] = r;"),
+               ("    gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;",
+                "    gbase[t] = (MODE == 1 || !c) ? 0ull : atomicAdd(&cursor[t], (unsigned long long)c);")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }

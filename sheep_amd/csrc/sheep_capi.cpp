@@ -47,7 +47,7 @@ static const KnobDef kKnobs[] = {
     {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
-    {"kb_pick", &Knobs::kb_pick},
+    {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
 };
 
 static Knobs g_knobs;

@@ -53,6 +53,7 @@ struct Knobs {
   int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
   int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
   int kb_pick = 1;       // SHEEP_KB_PICK: the giant's anchor picked on the device (0: rank B0 - 1)
+  int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
 };
 Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
 

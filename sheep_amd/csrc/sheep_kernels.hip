@@ -2431,10 +2431,16 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 // run (every chain of the bucket in flight at once, against the current union-find), and a
 // miss that reaches the giant sets its bit in gbits (nullable) when the bitmap's reference
 // vertex *gx lies in the anchor's component.
+// drop2: an in-bucket pair (a, b), B0 <= a < b, whose two ranks are both marked is dropped too:
+// both are ancestors of G through their own edges to G's component, so b is already an ancestor
+// of a without this edge (zip_step would stop it at its first step; here it costs two bitmap
+// reads in a flat stream instead of a lane of the zipper's queue).  A mark this launch has not
+// set yet only keeps a pair.
 __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept,
                              uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* bitmap,
                              uint32_t B0, uint32_t anchor, uint32_t* gbits,
-                             const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc) {
+                             const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc,
+                             int drop2) {
   const uint32_t nk = *n_kept;
   anchor = anchor_rank(anchor, anc);
   const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
@@ -2443,7 +2449,12 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
     const uint64_t it = kept[i];
     const uint32_t g = (uint32_t)it, b = (uint32_t)(it >> 32);
-    if (g >= B0) continue;
+    if (g >= B0) {
+      if (drop2 && RG != INV && b != INV && ((bitmap[g >> 5] >> (g & 31)) & 1u) &&
+          ((bitmap[b >> 5] >> (b & 31)) & 1u))
+        kept[i] = ~0ull;
+      continue;
+    }
     const uint32_t rt = uf_find<false>(uf, g);
     if (rt == RG) {
       const uint32_t bit = 1u << (b & 31);
@@ -2683,7 +2694,8 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   if (nonempty) {
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
-                         uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc);
+                         uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc,
+                         knobs().kb_drop);
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,

@@ -327,6 +327,7 @@ KB_KNOBS = [
     {"kb_pipe": 1, "kb_buckets": 512, "kb_rankb": 512},  # many narrow buckets
     {"kb_pick": 0},                                  # the host's anchor (rank B0 - 1) for every map
     {"kb_pick": 0, "kb_pipe": 0},
+    {"kb_drop": 0},                                  # in-bucket pairs of two marked ranks to the zipper
 ]
 
 

@@ -91,6 +91,7 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
                                                                     # the scatter path per rank
                                  {"bin_direct": 0},                 # edge pass + bin scatter
                                  {"kb_pick": 0},                    # the host's anchors
+                                 {"kb_drop": 0},
                                  {"kb_gbits": 0},                   # no giant bitmap in the maps
                                  {"part_overlap": 0}])              # no first pass beside the degrees
 def test_multi_local_front_half_options(oracle, gpu, options, env):
