@@ -1781,20 +1781,25 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
                                          const SpineInfo& sp = SpineInfo()) {
   if (STATS) c.steps++;
   if (!s.fresh) {
-    if (SPINE && !(s.flags & ZF_SPINE) && (s.x == sp.G || sp_marked(sp, s.x))) {
+    // the parent, the hint and (until the walk reaches the spine) x's mark word are loaded
+    // together: one memory latency per step, not two.  When the hint is taken the parent read
+    // is dropped; when the spine moves x, both are loaded again (once per pending edge).
+    const bool chk = SPINE && !(s.flags & ZF_SPINE);
+    const uint32_t mw = (chk && s.x >= sp.B0 && s.x < sp.B1) ? sp.bitmap[s.x >> 5] : 0u;
+    uint32_t pj = ld_parent<LOAD>(&parent[s.x]);
+    uint32_t j = JUMP ? jump[s.x] : 0u;
+    if (chk && (s.x == sp.G || ((mw >> (s.x & 31)) & 1u))) {
       s.flags |= ZF_SPINE;
       if (!(s.flags & ZF_KEEP) && sp_marked(sp, s.b)) return true;
       uint32_t y = sp_pred(sp, s.b, s.x);
       if (y != INV) {
         s.prev = INV;
         s.x = y;
+        pj = ld_parent<LOAD>(&parent[s.x]);
+        if (JUMP) j = jump[s.x];
       }
     }
-    // the hint and the parent are loaded together (one memory latency per step, not two);
-    // when the hint is taken the parent read is simply dropped
-    const uint32_t pj = ld_parent<LOAD>(&parent[s.x]);
     if (JUMP) {
-      const uint32_t j = jump[s.x];
       if (j > s.x && j < s.b) {
         if (s.prev != INV) jump[s.prev] = j;
         s.prev = s.x;
