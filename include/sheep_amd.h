@@ -79,7 +79,8 @@ int sheep_abi_version(void);
  * variables, read ONCE when the library first initialises a device; afterwards only these
  * calls change them (process-wide).  Names: degree, edge_part, part_overlap, seq_compact,
  * sort, kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, kb_defer, degb_plain, degb_hist, bin_tm,
- * bin_scatter, ep_plain, tree_stats, bin_direct, bin_slack, kb_pick, kb_drop.  -EINVAL for an unknown
+ * bin_scatter, ep_plain, tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum.  -EINVAL for an
+ * unknown
  * name. */
 int sheep_set_option(const char* name, long long value);
 int sheep_get_option(const char* name, long long* value);

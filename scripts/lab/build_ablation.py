@@ -204,10 +204,31 @@ void launch_edge_bin(""")],
     "p1noat": [("    out[gbase[d] + (j - tstart[d])] = r;", "    out[MODE == 1 ? tbase + j : gbase[d] + (j - tstart[d])] = r;"),
                ("    gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;",
                 "    gbase[t] = (MODE == 1 || !c) ? 0ull : atomicAdd(&cursor[t], (unsigned long long)c);")],
+    # (stats only, tree_stats=2) records with lo < B0, and those whose 64-rank block of the
+    # giant bitmap is all ones (what a per-block summary would answer without an L2 request)
+    "gsumstat": [("    if (STATS) misses += (uint64_t)__popc(miss);\n",
+                  "    if (STATS) misses += (uint64_t)__popc(miss);\n"
+                  "    if (STATS && use_bm) {\n"
+                  "      unsigned long long c13 = 0, c14 = 0;\n"
+                  "      for (int r = 0; r < R; ++r) {\n"
+                  "        const uint32_t a = (uint32_t)it[r];\n"
+                  "        if (((vmask >> r) & 1) && a < B0) {\n"
+                  "          ++c14;\n"
+                  "          if (gbits[(a >> 6) * 2] == ~0u && gbits[(a >> 6) * 2 + 1] == ~0u) ++c13;\n"
+                  "        }\n"
+                  "      }\n"
+                  "      if (c13) atomicAdd(&stats[13], c13);\n"
+                  "      if (c14) atomicAdd(&stats[14], c14);\n"
+                  "    }\n"),
+                 ],
+    # the zipper's LDS buffer of linked roots at 2048 entries (8 KB) instead of 512
+    "lcap2048": [("  constexpr uint32_t LCAP = 512;", "  constexpr uint32_t LCAP = 2048;")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }
 CAPI_PATCHES = {
+    "gsumstat": [("k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]);",
+                  "k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]);\n        fprintf(stderr, \"  gsum lo<B0 %llu in-full-blocks %llu\\n\", h[14], h[13]);")],
     "front": [('    if (tm) tm->mark("edge_pass");\n    HIP_CHECK(hipEventSynchronize(c.bins_ev));',
                '    if (tm) tm->mark("edge_pass");\n    HIP_CHECK(hipEventSynchronize(c.bins_ev));\n    HIP_CHECK(hipStreamSynchronize(s));\n    if (tm) tm->mark("bin_scatter");\n    return;')],
     "ptpad": [('c.scratch.get("part_ws", 1024 * 4)', 'c.scratch.get("part_ws", 16384 * 4)')],

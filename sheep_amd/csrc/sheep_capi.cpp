@@ -48,6 +48,7 @@ static const KnobDef kKnobs[] = {
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
+    {"kb_gsum", &Knobs::kb_gsum},
 };
 
 static Knobs g_knobs;
@@ -399,6 +400,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // giant bitmap (k_kb_map) and the two slots of its reference vertex (INV: none yet)
   uint32_t* gbits = (uint32_t*)c.scratch.get("kb_gbits", bm_words * 4);
   uint32_t* gx = (uint32_t*)c.scratch.get("kb_gx", 2 * 4);
+  // the giant summary the next map reads (written after each rebase)
+  uint32_t* gsum = (uint32_t*)c.scratch.get("kb_gsum", ((size_t)n_seq / 2048 + 2) * 4);
   // the giant's anchor of each map, picked on the device (two slots by bucket parity)
   uint32_t* anc = knobs().kb_pick ? (uint32_t*)c.scratch.get("kb_anchor", 2 * 4) : nullptr;
   if (anc) (void)hipMemsetAsync(anc, 0xFF, 2 * 4, s);
@@ -458,6 +461,9 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // union-find (map j-1 and apply j-1 complete); an apply uses the slot most recently written
   // on its stream.
   if (!knobs().kb_gbits) gbits = nullptr;
+  // the summary costs a launch per bucket: it pays on large inputs only (RMAT-26 tree 18.5 ->
+  // 16.7 ms; RMAT-22 3.25 -> 3.45 ms)
+  if (!gbits || !(knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))) gsum = nullptr;
   // the map leaves its union-find misses to the apply's refresh kernel (kb_defer)
   const bool defer = knobs().kb_defer != 0;
   hipStream_t sa = s;  // the applies and the rebases between them
@@ -466,10 +472,11 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       const uint32_t a = anchor_of(j);
       launch_kb_pick(uf, a == INV ? 0u : a + 1, anc + ((j - 1) & 1), anc + (j & 1), gbits, n_seq,
                      gx + ((j - 1) & 1), gx + (j & 1), sa);
-      return;
+    } else {
+      if (!gbits) return;
+      launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), sa);
     }
-    if (!gbits) return;
-    launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), sa);
+    if (gsum) launch_gb_sum(gbits, n_seq, gsum, sa);
   };
   auto map_k = [&](size_t k, hipStream_t st) {
     int p = par(k);
@@ -484,7 +491,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
                   seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
                   anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
                   lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer,
-                  st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr);
+                  st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr, k >= 1 ? gsum : nullptr);
     if (tm) tm->span_end(sp, st);
   };
   auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
@@ -881,6 +888,7 @@ struct Lockstep {
   // only spare finds) and the two slots of its reference vertex; rebased by the pick
   uint32_t* gbits = nullptr;
   uint32_t* gx = nullptr;
+  uint32_t* gsum = nullptr;  // the giant summary of the next map (launch_gb_sum, after the pick)
   ~Lockstep() {
     for (auto& e : pick_ev)
       if (e) (void)hipEventDestroy(e);
@@ -942,6 +950,9 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
       L.gx = (uint32_t*)sc.get("ls_gx", 2 * 4);
       HIP_CHECK(hipMemsetAsync(L.gbits, 0, bm_words * 4, s));
       HIP_CHECK(hipMemsetAsync(L.gx, 0xFF, 2 * 4, s));
+      // this rank's maps walk m records: the summary rule of tree_from_sorted
+      if (knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))
+        L.gsum = (uint32_t*)sc.get("ls_gsum", ((size_t)n_seq / 2048 + 2) * 4);
     }
   }
   launch_fill(L.parent, INV, n, s);
@@ -1089,7 +1100,8 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
                 L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
                 L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
                 L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
-                false, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr);
+                false, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr,
+                k >= 1 ? L.gsum : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
   if (n_kept_out) {
@@ -1134,6 +1146,8 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     launch_kb_pick(L.uf, a == INV ? 0u : a + 1, L.anc + (k & 1), L.anc + ((k + 1) & 1), L.gbits,
                    L.n_seq, L.gbits ? L.gx + (k & 1) : nullptr,
                    L.gbits ? L.gx + ((k + 1) & 1) : nullptr, s);
+    // map k+1 reads the summary; the next one is written by apply k+1, after map k+1 is done
+    if (L.gsum) launch_gb_sum(L.gbits, L.n_seq, L.gsum, s);
     HIP_CHECK(hipEventRecord(L.pick_ev[(k + 1) & 1], s));
     gslot = k + 1;
   }

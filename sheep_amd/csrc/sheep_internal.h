@@ -53,6 +53,8 @@ struct Knobs {
   int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
   int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
   int kb_pick = 1;       // SHEEP_KB_PICK: the giant's anchor picked on the device (0: rank B0 - 1)
+  int kb_gsum = -1;      // SHEEP_KB_GSUM: the map tests 64-rank "all in the giant" blocks in LDS
+                         //   first; -1 auto (from 2^27 records), 0, 1
   int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
 };
 Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
@@ -196,7 +198,11 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
                    bool defer /* misses kept as (b, a) for launch_kb_apply's refresh */,
                    hipStream_t s, const KbSegs* segs = nullptr,
-                   const uint32_t* anc = nullptr /* device-picked anchor (launch_kb_pick) */);
+                   const uint32_t* anc = nullptr /* device-picked anchor (launch_kb_pick) */,
+                   const uint32_t* gsum = nullptr /* giant summary (launch_gb_sum) */);
+// Giant summary for the next map (nothing writing gbits): bit q = ranks [64q, 64q + 64) all set
+// in gbits; (min(n_seq, 2^25) / 2048 + 1) words.
+void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStream_t s);
 // The giant's anchor for the next map, picked on the device among ranks [0, B0lim) (the
 // component holding most of an even sample; see sheep_kernels.hip), written to *anc_out (INV
 // when B0lim = 0); gbits (nullable): the bitmap is then rebased on it (launch_gb_rebase).

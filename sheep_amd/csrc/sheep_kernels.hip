@@ -2060,6 +2060,9 @@ static constexpr int KM_CHUNK = 8192;       // < 65536: the packed 16-bit counts
 static constexpr uint32_t KM_WIN = 32768;   // ranks
 static constexpr int KM_R = KM_CHUNK / KM_THREADS;  // records per lane per chunk
 static constexpr uint32_t KM_FLUSH = 65535 / KM_CHUNK;  // chunks per window flush at most
+// Giant summary words in the map's LDS (64 KB: ranks below 2^25).  The map's static LDS is
+// ~80 KB, so map + summary stays one block per CU and leaves ~16 KB beside it for the zipper.
+static constexpr uint32_t KM_GSUM = 16384;
 
 template <bool STATS>
 __global__ void __launch_bounds__(KM_THREADS)
@@ -2067,7 +2070,9 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
          uint32_t B0, int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
-         const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc) {
+         const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc,
+         const uint32_t* __restrict__ gsum, uint32_t gs_words) {
+  extern __shared__ uint32_t s_gsum[];  // gs_words words of the giant summary (dynamic LDS)
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -2093,6 +2098,10 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     for (uint32_t i = t; i < KM_WIN / 2; i += KM_THREADS) wcnt[i] = 0;
   if (bins)
     for (uint32_t i = t; i < nb; i += KM_THREADS) sbins[i] = bins[i];
+  // the summary covers ranks [0, gs_lim): bit q set = ranks [64q, 64q + 64) all have their
+  // giant bit (k_gb_sum, a snapshot taken before this map: bits are only ever added)
+  const uint32_t gs_lim = use_bm ? gs_words * 2048u : 0u;
+  for (uint32_t i = t; i < (use_bm ? gs_words : 0u); i += KM_THREADS) s_gsum[i] = gsum[i];
   __syncthreads();
   // Each block maps a contiguous run of chunks, so that consecutive chunks mostly share one
   // window (a bin): the window is flushed to global memory only when the next chunk's differs,
@@ -2174,7 +2183,10 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const uint32_t a = (uint32_t)it[r];
-      gw[r] = (use_bm && ((vmask >> r) & 1) && a < B0) ? gbits[a >> 5] : 0u;
+      const bool t_ = use_bm && ((vmask >> r) & 1) && a < B0;
+      // most lo ranks lie in 64-rank blocks that are all in the giant: answered from LDS
+      const bool full = t_ && a < gs_lim && ((s_gsum[a >> 11] >> ((a >> 6) & 31)) & 1u);
+      gw[r] = full ? ~0u : (t_ ? gbits[a >> 5] : 0u);
     }
     const bool more = j + 1 < j1;
     if (more) fetch(j + 1);  // issued after the bitmap loads
@@ -2302,6 +2314,31 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
 // and the previous apply are complete): keep the bitmap's reference vertex X if it lies in the
 // component of this map's anchor, else move X to the anchor and clear the bitmap.  X is read
 // from one slot and written to the other (every block reads before block 0 writes).
+// The giant summary: bit q of gsum = ranks [64q, 64q + 64) all have their giant bit (one lane
+// per 64-rank block, ballot-assembled words).  Run with nothing writing gbits (before a map,
+// after the rebase).
+__global__ void k_gb_sum(const uint32_t* __restrict__ gbits, uint32_t nblocks, uint32_t* gsum) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  bool full = false;
+  if (q < nblocks) {
+    const uint2 w = *(const uint2*)(gbits + 2 * (size_t)q);
+    full = w.x == ~0u && w.y == ~0u;
+  }
+  const uint64_t bal = __ballot(full);
+  const int lane = threadIdx.x & 63;
+  if (q - lane < nblocks) {  // the wave's first block exists
+    if (lane == 0) gsum[q >> 5] = (uint32_t)bal;
+    if (lane == 32) gsum[q >> 5] = (uint32_t)(bal >> 32);
+  }
+}
+
+void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStream_t s) {
+  const uint32_t nblocks = std::min<uint32_t>(n_seq / 64, KM_GSUM * 32);
+  if (nblocks == 0) return;
+  hipLaunchKernelGGL(k_gb_sum, dim3((nblocks + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, gbits, nblocks,
+                     gsum);
+}
+
 __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf, uint32_t anchor,
                             const uint32_t* __restrict__ gx_rd, uint32_t* gx_wr) {
   const uint32_t X = *gx_rd;
@@ -2486,7 +2523,7 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
                          uint32_t* jump, unsigned long long* stats, uint32_t* linked,
                          uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
                          uint32_t qchunk, const uint32_t* __restrict__ anc) {
-  constexpr uint32_t LCAP = 2048;
+  constexpr uint32_t LCAP = 2048;  // (512: RMAT-26 tree 16.7 -> 18.2 ms)
   __shared__ uint32_t lbuf[LCAP];
   __shared__ uint32_t lcnt, lbase;
   if (threadIdx.x == 0) lcnt = 0;
@@ -2650,7 +2687,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
                    const uint32_t* gx, bool defer, hipStream_t s, const KbSegs* segs,
-                   const uint32_t* anc) {
+                   const uint32_t* anc, const uint32_t* gsum) {
   // segs: e_begin / e_end bound the bucket's records (the capacity of its bins)
   if (e_end <= e_begin) return;
   KbSegs sg{};
@@ -2664,9 +2701,12 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   // phase 28.6 / 27.6 / 31.0 / 29.8 ms at 512 / 256 / 320 / 384 blocks; 192: 29.7).
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-  hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), 0, s, items, e_begin, e_end, sg, B0, gshift,
-                     uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx, (int)defer, anc);
+  // the giant summary of ranks [0, B0) in dynamic LDS, at most KM_GSUM words
+  const uint32_t gs_words =
+      (gsum && gx) ? std::min<uint32_t>((B0 + 2047) / 2048, KM_GSUM) : 0u;
+  hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), gs_words * 4, s, items, e_begin, e_end, sg,
+                     B0, gshift, uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
+                     gx ? gbits : nullptr, gx, (int)defer, anc, gsum, gs_words);
 }
 
 void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,

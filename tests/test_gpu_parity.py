@@ -328,6 +328,8 @@ KB_KNOBS = [
     {"kb_pick": 0},                                  # the host's anchor (rank B0 - 1) for every map
     {"kb_pick": 0, "kb_pipe": 0},
     {"kb_drop": 0},                                  # in-bucket pairs of two marked ranks to the zipper
+    {"kb_gsum": 0},                                  # no LDS giant summary in the map
+    {"kb_gsum": 1},                                  # the summary at every size (auto: 2^27 records)
 ]
 
 

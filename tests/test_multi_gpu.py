@@ -93,6 +93,7 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
                                  {"kb_pick": 0},                    # the host's anchors
                                  {"kb_drop": 0},
                                  {"kb_gbits": 0},                   # no giant bitmap in the maps
+                                 {"kb_gsum": 1},                    # the LDS giant summary
                                  {"part_overlap": 0}])              # no first pass beside the degrees
 def test_multi_local_front_half_options(oracle, gpu, options, env):
     """The multi-rank driver under the front-half / anchor options: the same tree (R-MAT 19,
