@@ -48,6 +48,13 @@ __device__ __forceinline__ uint64_t ev_key(uint32_t X, uint32_t Y, const int16_t
   return ((uint64_t)v << 32) | X;  // the radix sort orders the high word: first by part
 }
 
+// Workgroup barrier that first drains the wave's LDS operations (see block_sync in
+// sheep_kernels.hip: a plain __syncthreads() once lost no-return LDS adds on a loop exit).
+__device__ __forceinline__ void ev_block_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __syncthreads();
+}
+
 // (part << 32 | X) -> (X << 32 | part) between the two stable sorts; ~0 stays ~0.
 __global__ void k_ev_swap(uint64_t* keys, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -94,7 +101,7 @@ __global__ void k_ev_records(const uint2* __restrict__ uv, uint64_t m, uint32_t 
   const bool lds = k <= EV_LDS_PARTS;
   if (lds)
     for (uint32_t i = threadIdx.x; i < 3 * k; i += blockDim.x) lh[i] = 0;
-  __syncthreads();
+  ev_block_sync();
   unsigned long long cut = 0, self = 0;
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
        e += (uint64_t)gridDim.x * blockDim.x) {
@@ -129,7 +136,7 @@ __global__ void k_ev_records(const uint2* __restrict__ uv, uint64_t m, uint32_t 
     if (self) atomicAdd(&cnt[1], self);
   }
   if (lds) {
-    __syncthreads();
+    ev_block_sync();
     for (uint32_t i = threadIdx.x; i < 3 * k; i += blockDim.x)
       if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
   }
@@ -143,7 +150,7 @@ __global__ void k_ev_nodes(const uint32_t* __restrict__ deg, uint32_t n_ids,
   const bool lds = k <= EV_LDS_PARTS;
   if (lds)
     for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) lh[i] = 0;
-  __syncthreads();
+  ev_block_sync();
   unsigned long long nodes = 0;
   for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_ids; v += gridDim.x * blockDim.x) {
     if (!deg[v]) continue;
@@ -155,7 +162,7 @@ __global__ void k_ev_nodes(const uint32_t* __restrict__ deg, uint32_t n_ids,
   for (int o = 32; o > 0; o >>= 1) nodes += __shfl_down(nodes, o);
   if ((threadIdx.x & 63) == 0 && nodes) atomicAdd(&cnt[2], nodes);
   if (lds) {
-    __syncthreads();
+    ev_block_sync();
     for (uint32_t i = threadIdx.x; i < k; i += blockDim.x)
       if (lh[i]) atomicAdd(&vbal[i], (unsigned long long)lh[i]);
   }

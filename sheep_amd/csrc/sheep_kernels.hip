@@ -182,6 +182,15 @@ void launch_fill(uint32_t* p, uint32_t value, uint64_t n, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 // Exclusive scan (u32), TILE elements per block: reduce -> scan of block sums -> downsweep.
 // ---------------------------------------------------------------------------------------
+// Workgroup barrier that first drains the wave's LDS operations.  __syncthreads() alone was
+// once compiled without that wait on a loop exit (k_degb_hist16: the last no-return ds_add of
+// the counting loop could land after another wave's read behind the barrier, which lost or
+// moved counts run to run — measured on the twitter shape), so every barrier here waits.
+__device__ __forceinline__ void block_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt and expcnt left at their maxima
+  __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   int lane = threadIdx.x & 63;
   for (int o = 1; o < 64; o <<= 1) {
@@ -200,14 +209,14 @@ __device__ uint32_t block_scan_tile(uint32_t* tile, uint32_t* wsum) {
   for (int i = 0; i < ITEMS; ++i) { local[i] = tile[t * ITEMS + i]; sum += local[i]; }
   uint32_t incl = wave_incl_scan(sum);
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  block_sync();
   uint32_t wbase = 0, total = 0;
 #pragma unroll
   for (int i = 0; i < BLOCK / 64; ++i) { if (i < w) wbase += wsum[i]; total += wsum[i]; }
   uint32_t run = wbase + incl - sum;
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) { tile[t * ITEMS + i] = run; run += local[i]; }
-  __syncthreads();
+  block_sync();
   return total;
 }
 
@@ -221,7 +230,7 @@ __global__ void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n, uint3
   for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
   __shared__ uint32_t ws[BLOCK / 64];
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (int i = 0; i < BLOCK / 64; ++i) t += ws[i];
@@ -238,7 +247,7 @@ __global__ void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restric
     uint64_t idx = base + (uint64_t)i * BLOCK + threadIdx.x;
     tile[i * BLOCK + threadIdx.x] = idx < n ? in[idx] : 0;
   }
-  __syncthreads();
+  block_sync();
   block_scan_tile(tile, wsum);
   uint32_t off = offsets ? offsets[blockIdx.x] : 0;
   for (int i = 0; i < ITEMS; ++i) {
@@ -295,7 +304,7 @@ __device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, ui
     zeros += (uint32_t)__shfl_xor((int)zeros, o);
   }
   if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = mx; szr[threadIdx.x >> 6] = zeros; }
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) {
     for (int i = 1; i < DEGB_THREADS / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; }
     if (mx) atomicMax(&stats[0], mx);
@@ -322,7 +331,7 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
   __shared__ uint32_t yh[256];  // y digits of the later rank-gather partition (nullable yhist)
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) yh[i] = 0;
-  __syncthreads();
+  block_sync();
   const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
   const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
   constexpr int U = 8;  // records loaded per thread before use (bytes in flight)
@@ -343,7 +352,7 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
       if (yhist) atomicAdd(&yh[part_digit(e[u].y, psh)], 1u);
     }
   }
-  __syncthreads();
+  block_sync();
   if (yhist)
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
       if (yh[i]) atomicAdd(&yhist[i], yh[i]);
@@ -368,14 +377,14 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
   }
   uint32_t incl = wave_incl_scan(cnt);
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  block_sync();
   if (t < (int)NB) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     start[t] = add + incl - cnt;
     cur[t] = add + incl - cnt;
   }
-  __syncthreads();
+  block_sync();
   const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
   const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
   constexpr int U = 8;
@@ -397,7 +406,7 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
       if (loop && selfc) atomicAdd(&selfc[e.x], 1u);
     }
   }
-  __syncthreads();
+  block_sync();
   // each wave writes whole bucket runs
   for (uint32_t b = w; b < NB; b += DEGB_THREADS / 64) {
     uint32_t s0 = start[b], n = cur[b] - s0;
@@ -415,7 +424,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) cnt[i] = 0;
-  __syncthreads();
+  block_sync();
   // bstart (tile-major counts): bucket starts and the total; else the digit-major offsets
   const uint64_t last = (uint64_t)NB * nchunks - 1;
   uint64_t s0 = bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
@@ -461,7 +470,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
       }
     }
   }
-  __syncthreads();
+  block_sync();
   uint64_t g0 = ((uint64_t)b << SH) + (uint64_t)h * span;
   uint32_t mx = 0, zeros = 0;
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x)
@@ -499,7 +508,7 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
   for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
     const uint64_t g1 = min(g0 + 65535, s1);
     for (uint32_t i = threadIdx.x; i < 32768; i += DEGB_THREADS) pk[i] = 0;
-    __syncthreads();
+    block_sync();
     for (uint64_t i0 = g0 & ~7ull; i0 < g1; i0 += 8 * V * DEGB_THREADS) {
       uint4 q[V];
 #pragma unroll
@@ -533,13 +542,13 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
         }
       }
     }
-    __syncthreads();
+    block_sync();
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
       const uint32_t id = (uint32_t)k * DEGB_THREADS + threadIdx.x;
       acc[k] += (pk[id >> 1] >> (16 * (id & 1))) & 0xFFFFu;
     }
-    __syncthreads();
+    block_sync();
   }
   const uint64_t base = (uint64_t)b << 16;
   uint32_t mx = 0, zeros = 0;
@@ -701,7 +710,7 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
   __shared__ uint32_t hist[NBIN];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (uint32_t i = t; i < NBIN; i += RS_THREADS) hist[i] = 0;
-  __syncthreads();
+  block_sync();
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (64 * RS_ITEMS) + lane;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t it[RS_ITEMS];
@@ -717,7 +726,7 @@ k_rsort_count(const uint64_t* __restrict__ in, uint64_t n, int shift, uint32_t* 
     uint64_t match = digit_match<DB>(d, valid);  // one LDS add per distinct digit (skewed keys)
     if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
   }
-  __syncthreads();
+  block_sync();
   for (uint32_t i = t; i < NBIN; i += RS_THREADS)
     counts[TM ? (uint64_t)blockIdx.x * NBIN + i : (uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
@@ -751,7 +760,7 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   for (uint32_t i = lane; i < NBIN; i += 64) whist[w][i] = 0;
   if (BINS) {
     for (uint32_t i = t; i < nb; i += RS_THREADS) sb[i] = bins[i];
-    __syncthreads();
+    block_sync();
   }
   uint32_t dg[RS_ITEMS];
   uint64_t item[RS_ITEMS];
@@ -774,7 +783,7 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
     rk[k] = prev + before;
     if (valid && before == 0) whist[w][d] = prev + (uint32_t)__popcll(match);
   }
-  __syncthreads();
+  block_sync();
   // per-wave counts -> per-wave exclusive offsets inside each digit; tile digit totals -> tstart
   for (uint32_t dd = t; dd < NBIN; dd += RS_THREADS) {
     uint32_t s = 0;
@@ -784,13 +793,13 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
     if (lane == 63) wsum[w] = incl;
     tstart[dd] = incl - s;
   }
-  __syncthreads();
+  block_sync();
   if (t < (int)NBIN) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     if (wbase + (uint32_t)k * 64 < tile_n) {
@@ -799,7 +808,7 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
       if (BINS) stage_d[tstart[d] + whist[w][d] + rk[k]] = (uint16_t)d;
     }
   }
-  __syncthreads();
+  block_sync();
   for (uint32_t j = t; j < tile_n; j += RS_THREADS) {
     uint64_t it = stage[j];
     uint32_t d = BINS ? (uint32_t)stage_d[j] : digit(it);
@@ -863,7 +872,7 @@ k_tm_scan_groups(uint32_t* __restrict__ gsum, uint32_t ngroups, uint32_t NC, uin
     }
   const uint32_t incl = wave_incl_scan(run);
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  block_sync();
   uint32_t add = 0;
   for (uint32_t i = 0; i < w; ++i) add += wsum[i];
   if (d < nb) bin_start[d] = add + incl - run;
@@ -931,29 +940,29 @@ k_bin_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint6
     it[k] = j < tile_n ? in[tbase + j] : 0ull;
     dg[k] = j < tile_n ? digits[tbase + j] : 0u;
   }
-  __syncthreads();
+  block_sync();
   uint32_t li[IT];
 #pragma unroll
   for (int k = 0; k < IT; ++k)
     if ((uint32_t)k * NT + t < tile_n) li[k] = atomicAdd(&hist[dg[k]], 1u);
-  __syncthreads();
+  block_sync();
   if (t < 512) {
     const uint32_t c = hist[t];
     const uint32_t incl = wave_incl_scan(c);
     if (lane == 63) wsum[w] = incl;
     tstart[t] = incl - c;
   }
-  __syncthreads();
+  block_sync();
   if (t < 512) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < IT; ++k)
     if ((uint32_t)k * NT + t < tile_n) stage[tstart[dg[k]] + li[k]] = it[k];
-  __syncthreads();
+  block_sync();
   for (uint32_t d = w; d < 512; d += NT / 64) {
     const uint32_t s0 = tstart[d], c = hist[d];
     const uint64_t g = goff[d];
@@ -1106,7 +1115,7 @@ k_nz_count(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* __restrict__ 
   for (int k = 0; k < 4; ++k) c += (base + k < n && deg[base + k] != 0);
   for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
   if ((t & 63) == 0) wsum[t >> 6] = c;
-  __syncthreads();
+  block_sync();
   if (t == 0) {
     uint32_t sum = 0;
     for (int i = 0; i < 16; ++i) sum += wsum[i];
@@ -1127,7 +1136,7 @@ k_pack_nz(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __restri
   }
   const uint32_t incl = wave_incl_scan(c);
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  block_sync();
   uint32_t pos = bofs[blockIdx.x] + incl - c;
   for (uint32_t i = 0; i < w; ++i) pos += wsum[i];
 #pragma unroll
@@ -1305,7 +1314,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
       ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
     }
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     uint64_t idx = base + (uint64_t)k * 64;
@@ -1335,7 +1344,7 @@ k_edge_pass_tiles(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __re
       if (valid && (match & lt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(match));
     }
   }
-  __syncthreads();
+  block_sync();
   for (uint32_t i = t; i < NBIN; i += RS_THREADS)
     counts[TM ? (uint64_t)blockIdx.x * NBIN + i : (uint64_t)i * ntiles + blockIdx.x] = hist[i];
 }
@@ -1426,7 +1435,7 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
       ry[k] = (g && e[k].y < n_rank) ? rank[e[k].y] : INV;
     }
   }
-  __syncthreads();
+  block_sync();
   uint64_t item[IT];
   uint32_t pk[IT];  // bin << 16 | index within the tile's run of the bin; ~0u: not stored
 #pragma unroll
@@ -1453,7 +1462,7 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
       pk[k] = (d << 16) | atomicAdd(&hist[d], 1u);
     }
   }
-  __syncthreads();
+  block_sync();
   if (t < 512) {
     const uint32_t c = hist[t];
     const uint32_t incl = wave_incl_scan(c);
@@ -1469,17 +1478,17 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
     }
     gbase[t] = g;
   }
-  __syncthreads();
+  block_sync();
   if (t < 512) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < IT; ++k)
     if (pk[k] != ~0u) stage[tstart[pk[k] >> 16] + (pk[k] & 0xFFFFu)] = item[k];
-  __syncthreads();
+  block_sync();
   for (uint32_t d = w; d < 512; d += NT / 64) {
     const uint32_t c = hist[d];
     const unsigned long long g = gbase[d];
@@ -1530,11 +1539,11 @@ __global__ void __launch_bounds__(PT_THREADS)
 k_part_count(const uint2* __restrict__ uv, uint64_t m, int sh, uint32_t* __restrict__ ghist) {
   __shared__ uint32_t hist[256];
   for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS) hist[i] = 0;
-  __syncthreads();
+  block_sync();
   for (uint64_t i = (uint64_t)blockIdx.x * PT_THREADS + threadIdx.x; i < m;
        i += (uint64_t)gridDim.x * PT_THREADS)
     atomicAdd(&hist[part_digit(uv[i].y, sh)], 1u);
-  __syncthreads();
+  block_sync();
   for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS)
     if (hist[i]) atomicAdd(&ghist[i], hist[i]);
 }
@@ -1544,12 +1553,12 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
   __shared__ unsigned long long s[256];
   uint32_t t = threadIdx.x;
   s[t] = hist[t];
-  __syncthreads();
+  block_sync();
   if (t == 0) {
     unsigned long long run = 0;
     for (int i = 0; i < 256; ++i) { unsigned long long v = s[i]; s[i] = run; run += v; }
   }
-  __syncthreads();
+  block_sync();
   cursor[t] = s[t];
   hist[t] = 0;
 }
@@ -1589,7 +1598,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
       rec[k] = ((uint64_t)v << 32) | x;
     }
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
     if ((uint32_t)k * NT + t < tile_n) {
@@ -1598,7 +1607,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
       if (MODE == 0) atomicAdd(&hx[part_digit((uint32_t)rec[k], sh)], 1u);
     }
   }
-  __syncthreads();
+  block_sync();
   if (t < 256) {
     uint32_t c = hist[t];
     uint32_t incl = wave_incl_scan(c);
@@ -1607,13 +1616,13 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
     gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;
     if (MODE == 0 && hx[t]) atomicAdd(&xhist[t], hx[t]);
   }
-  __syncthreads();
+  block_sync();
   if (t < 256) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
   }
-  __syncthreads();
+  block_sync();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
     if ((uint32_t)k * NT + t < tile_n) {
@@ -1621,7 +1630,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
       stage[tstart[part_digit(key, sh)] + li[k]] = rec[k];
     }
   }
-  __syncthreads();
+  block_sync();
   for (uint32_t j = t; j < tile_n; j += NT) {
     uint64_t r = stage[j];
     uint32_t d = part_digit(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
@@ -2102,7 +2111,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
   // giant bit (k_gb_sum, a snapshot taken before this map: bits are only ever added)
   const uint32_t gs_lim = use_bm ? gs_words * 2048u : 0u;
   for (uint32_t i = t; i < (use_bm ? gs_words : 0u); i += KM_THREADS) s_gsum[i] = gsum[i];
-  __syncthreads();
+  block_sync();
   // Each block maps a contiguous run of chunks, so that consecutive chunks mostly share one
   // window (a bin): the window is flushed to global memory only when the next chunk's differs,
   // after KM_FLUSH chunks (the packed 16-bit counts must not carry), and at the end.
@@ -2119,7 +2128,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     s_s0[0] = e_begin;
     s_len[0] = (uint32_t)(e_end - e_begin);
   }
-  __syncthreads();
+  block_sync();
   if (w == 0) {
     uint32_t run = 0;
     for (uint32_t b0 = 0; b0 < nseg; b0 += 64) {
@@ -2131,7 +2140,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     }
     if (lane == 0) s_cp[nseg] = run;
   }
-  __syncthreads();
+  block_sync();
   const uint32_t total = s_cp[nseg];
   const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
   const uint32_t j0 = min(blockIdx.x * per, total), j1 = min(j0 + per, total);
@@ -2265,7 +2274,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       window(nh0, nbl, nbase, nend);
       flush = nbase != bbase || nend != gend;
     }
-    __syncthreads();
+    block_sync();
     if (flush) {
       since_flush = 0;
       for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) {
@@ -2291,7 +2300,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       for (int i = 0; i < KM_THREADS / 64; ++i) { uint32_t v = woff[i]; woff[i] = run; run += v; }
       woff[KM_THREADS / 64] = run ? atomicAdd(n_kept, run) : 0u;
     }
-    __syncthreads();
+    block_sync();
     uint32_t pos = woff[KM_THREADS / 64] + woff[w];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -2379,7 +2388,7 @@ k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_p
     roots[t] = r;
     const uint32_t prev = *anc_prev;
     const uint32_t rp = (prev != INV && prev < B0lim) ? uf_find_ro(uf, prev) : INV;
-    __syncthreads();
+    block_sync();
     uint32_t cnt = 0;  // samples in this thread's component
     for (int u = 0; u < KP; ++u) cnt += roots[u] == r;
     uint32_t key = (cnt << 16) | (uint32_t)t;  // most samples, then the highest thread
@@ -2389,7 +2398,7 @@ k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_p
       cp = max(cp, (uint32_t)__shfl_xor((int)cp, o));
     }
     if (lane == 0) { wkey[w] = key; wcp[w] = cp; }
-    __syncthreads();
+    block_sync();
     if (t == 0) {
       uint32_t bk = 0, bp = 0;
       for (int i = 0; i < KP / 64; ++i) { bk = max(bk, wkey[i]); bp = max(bp, wcp[i]); }
@@ -2397,7 +2406,7 @@ k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_p
       const uint32_t bs = bt == KP - 1 ? B0lim - 1 : (uint32_t)(((uint64_t)bt * B0lim) / KP);
       s_anchor = (rp != INV && bp >= 3 && bp + 4 >= bc) ? prev : (bc >= 3 ? bs : B0lim - 1);
     }
-    __syncthreads();
+    block_sync();
     anchor = s_anchor;
   }
   if (blockIdx.x == 0 && t == 0) *anc_out = anchor;
@@ -2527,7 +2536,7 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   __shared__ uint32_t lbuf[LCAP];
   __shared__ uint32_t lcnt, lbase;
   if (threadIdx.x == 0) lcnt = 0;
-  __syncthreads();
+  block_sync();
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
@@ -2553,10 +2562,10 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
     tree_queue_body<0, 1, STATS, true, false>(src, nk, parent, jump, stats, rec, qchunk);
   }
   // the block's staged linked roots: one reservation, a coalesced copy
-  __syncthreads();
+  block_sync();
   const uint32_t n = min(lcnt, LCAP);
   if (threadIdx.x == 0) lbase = n ? atomicAdd(n_linked, n) : 0u;
-  __syncthreads();
+  block_sync();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) linked[lbase + i] = lbuf[i];
 }
 

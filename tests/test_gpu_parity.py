@@ -419,12 +419,13 @@ def test_degree_64k_id_buckets(oracle, api, options, hist):
 
     options(degb_hist=int(hist), degree=2)
     rng = np.random.default_rng(7)
-    n_ids = (1 << 26) + 5
-    m = 1 << 20
+    n_ids = (1 << 26) - 5  # above 2^26 the bucketed path does not apply (global atomics)
+    m = 1 << 21
     uv = rng.integers(0, n_ids, size=(m, 2)).astype(np.uint32)
-    dense = rng.random(m) < 0.25  # a quarter of the records inside bucket 3
+    # 40 % of the records inside bucket 3: ~1.8 M endpoints counted in many 65535-entry folds
+    dense = rng.random(m) < 0.4
     uv[dense] = (3 << 16) + rng.integers(0, 4000, size=(int(dense.sum()), 2)).astype(np.uint32)
-    hub = rng.random(m) < 0.12  # ~126K occurrences of one id of bucket 3
+    hub = rng.random(m) < 0.12  # ~250K occurrences of one id of bucket 3
     uv[hub, 0] = (3 << 16) + 17
     loops = rng.random(m) < 0.03
     uv[loops, 1] = uv[loops, 0]
