@@ -201,7 +201,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    const uint32_t* anc = nullptr /* device-picked anchor (launch_kb_pick) */,
                    const uint32_t* gsum = nullptr /* giant summary (launch_gb_sum) */);
 // Giant summary for the next map (nothing writing gbits): bit q = ranks [64q, 64q + 64) all set
-// in gbits; (min(n_seq, 2^25) / 2048 + 1) words.
+// in gbits; (n_seq / 2048 + 1) words.
 void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStream_t s);
 // The giant's anchor for the next map, picked on the device among ranks [0, B0lim) (the
 // component holding most of an even sample; see sheep_kernels.hip), written to *anc_out (INV

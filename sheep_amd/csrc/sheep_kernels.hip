@@ -2080,7 +2080,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
          const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc,
-         const uint32_t* __restrict__ gsum, uint32_t gs_words) {
+         const uint32_t* __restrict__ gsum, uint32_t gs_words, uint32_t gs_w0) {
   extern __shared__ uint32_t s_gsum[];  // gs_words words of the giant summary (dynamic LDS)
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
@@ -2107,10 +2107,11 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     for (uint32_t i = t; i < KM_WIN / 2; i += KM_THREADS) wcnt[i] = 0;
   if (bins)
     for (uint32_t i = t; i < nb; i += KM_THREADS) sbins[i] = bins[i];
-  // the summary covers ranks [0, gs_lim): bit q set = ranks [64q, 64q + 64) all have their
-  // giant bit (k_gb_sum, a snapshot taken before this map: bits are only ever added)
-  const uint32_t gs_lim = use_bm ? gs_words * 2048u : 0u;
-  for (uint32_t i = t; i < (use_bm ? gs_words : 0u); i += KM_THREADS) s_gsum[i] = gsum[i];
+  // the summary covers ranks [gs_lo, gs_hi), the KM_GSUM words below B0 (all of them when
+  // B0 <= 2^25): bit q set = ranks [64q, 64q + 64) all have their giant bit (k_gb_sum, a
+  // snapshot taken before this map: bits are only ever added)
+  const uint32_t gs_lo = gs_w0 * 2048u, gs_hi = use_bm ? gs_lo + gs_words * 2048u : 0u;
+  for (uint32_t i = t; i < (use_bm ? gs_words : 0u); i += KM_THREADS) s_gsum[i] = gsum[gs_w0 + i];
   block_sync();
   // Each block maps a contiguous run of chunks, so that consecutive chunks mostly share one
   // window (a bin): the window is flushed to global memory only when the next chunk's differs,
@@ -2194,7 +2195,8 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       const uint32_t a = (uint32_t)it[r];
       const bool t_ = use_bm && ((vmask >> r) & 1) && a < B0;
       // most lo ranks lie in 64-rank blocks that are all in the giant: answered from LDS
-      const bool full = t_ && a < gs_lim && ((s_gsum[a >> 11] >> ((a >> 6) & 31)) & 1u);
+      const bool full = t_ && a >= gs_lo && a < gs_hi &&
+                        ((s_gsum[(a - gs_lo) >> 11] >> ((a >> 6) & 31)) & 1u);
       gw[r] = full ? ~0u : (t_ ? gbits[a >> 5] : 0u);
     }
     const bool more = j + 1 < j1;
@@ -2326,26 +2328,26 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
 // The giant summary: bit q of gsum = ranks [64q, 64q + 64) all have their giant bit (one lane
 // per 64-rank block, ballot-assembled words).  Run with nothing writing gbits (before a map,
 // after the rebase).
-__global__ void k_gb_sum(const uint32_t* __restrict__ gbits, uint32_t nblocks, uint32_t* gsum) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_gb_sum(const uint32_t* __restrict__ gbits, uint32_t nfull, uint32_t nwords,
+                         uint32_t* gsum) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;  // one 64-rank block per lane
   bool full = false;
-  if (q < nblocks) {
+  if (q < nfull) {  // complete blocks only: a partial last block reads as not full
     const uint2 w = *(const uint2*)(gbits + 2 * (size_t)q);
     full = w.x == ~0u && w.y == ~0u;
   }
   const uint64_t bal = __ballot(full);
   const int lane = threadIdx.x & 63;
-  if (q - lane < nblocks) {  // the wave's first block exists
-    if (lane == 0) gsum[q >> 5] = (uint32_t)bal;
-    if (lane == 32) gsum[q >> 5] = (uint32_t)(bal >> 32);
-  }
+  if ((lane == 0 || lane == 32) && (q >> 5) < nwords)  // every word a map may read is written
+    gsum[q >> 5] = lane ? (uint32_t)(bal >> 32) : (uint32_t)bal;
 }
 
 void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStream_t s) {
-  const uint32_t nblocks = std::min<uint32_t>(n_seq / 64, KM_GSUM * 32);
-  if (nblocks == 0) return;
-  hipLaunchKernelGGL(k_gb_sum, dim3((nblocks + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, gbits, nblocks,
-                     gsum);
+  const uint32_t nwords = (n_seq + 2047) / 2048;  // the words of ranks [0, n_seq)
+  if (nwords == 0) return;
+  const uint32_t lanes = nwords * 32;
+  hipLaunchKernelGGL(k_gb_sum, dim3((lanes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, gbits, n_seq / 64,
+                     nwords, gsum);
 }
 
 __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf, uint32_t anchor,
@@ -2710,12 +2712,14 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   // phase 28.6 / 27.6 / 31.0 / 29.8 ms at 512 / 256 / 320 / 384 blocks; 192: 29.7).
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
   auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
-  // the giant summary of ranks [0, B0) in dynamic LDS, at most KM_GSUM words
-  const uint32_t gs_words =
-      (gsum && gx) ? std::min<uint32_t>((B0 + 2047) / 2048, KM_GSUM) : 0u;
+  // the giant summary of the highest KM_GSUM words of ranks below B0 (the lo ends of most
+  // records: a vertex is the lo end of its edges to higher-degree vertices) in dynamic LDS
+  const uint32_t w_end = (B0 + 2047) / 2048;
+  const uint32_t gs_words = (gsum && gx) ? std::min<uint32_t>(w_end, KM_GSUM) : 0u;
+  const uint32_t gs_w0 = w_end - gs_words;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), gs_words * 4, s, items, e_begin, e_end, sg,
                      B0, gshift, uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx, (int)defer, anc, gsum, gs_words);
+                     gx ? gbits : nullptr, gx, (int)defer, anc, gsum, gs_words, gs_w0);
 }
 
 void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,
