@@ -223,6 +223,10 @@ void launch_edge_bin(""")],
                  ],
     # the zipper's LDS buffer of linked roots at 2048 entries (8 KB) instead of 512
     "lcap2048": [("  constexpr uint32_t LCAP = 512;", "  constexpr uint32_t LCAP = 2048;")],
+    # map grids of 3/4 and 1/2 of the CUs (with the LDS giant summary the map needs fewer
+    # L2 requests; fewer map blocks leave more of the chip to the apply beside it)
+    "mg34": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, device_cus() * 3 / 4);")],
+    "mgh": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, device_cus() / 2);")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }
