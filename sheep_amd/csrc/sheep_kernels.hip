@@ -2260,9 +2260,13 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
         if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
         else atomicAdd(&cnt[b], 1u);
       }
-      if (gi) {
-        if (o < span) atomicOr(&wbits[o >> 5], 1u << (o & 31));
-        else atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+      if (gi) {  // a hub's records repeat its mark: test first (a read of one word is a
+                 // broadcast, same-word atomics from a wave serialise)
+        if (o < span) {
+          if (!((wbits[o >> 5] >> (o & 31)) & 1u)) atomicOr(&wbits[o >> 5], 1u << (o & 31));
+        } else if (!((bitmap[b >> 5] >> (b & 31)) & 1u)) {
+          atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+        }
       }
       const bool k2 = valid && !gi;
       it[r] = k2 ? (((uint64_t)b << 32) | g) : ~0ull;
