@@ -227,6 +227,22 @@ void launch_edge_bin(""")],
     # L2 requests; fewer map blocks leave more of the chip to the apply beside it)
     "mg34": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, device_cus() * 3 / 4);")],
     "mgh": [("std::min<uint64_t>(chunks, device_cus());", "std::min<uint64_t>(chunks, device_cus() / 2);")],
+    # hi counts: runs of equal hi in consecutive lanes added once by the run's first lane
+    "cntrun": [("""      if (valid && cnt) {
+        if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
+        else atomicAdd(&cnt[b], 1u);
+      }""", """      {
+        const uint32_t bk = valid ? b : INV;
+        const uint32_t bp = (uint32_t)__shfl_up((int)bk, 1);
+        const bool lead = valid && (lane == 0 || bp != bk);
+        const uint64_t brk = __ballot(!valid || lead);
+        const uint64_t after = lane == 63 ? 0ull : (brk >> (lane + 1));
+        const uint32_t len = after ? (uint32_t)__ffsll((unsigned long long)after) : (uint32_t)(64 - lane);
+        if (lead && cnt) {
+          if (o < span) atomicAdd(&wcnt[o >> 1], len << (16 * (o & 1)));
+          else atomicAdd(&cnt[b], len);
+        }
+      }""")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }
