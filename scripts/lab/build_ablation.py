@@ -243,6 +243,17 @@ void launch_edge_bin(""")],
           else atomicAdd(&cnt[b], len);
         }
       }""")],
+    # 64K-id histogram: leader matching only in the long (hub) runs, plain adds elsewhere
+    "h16hot": [("""  uint32_t acc[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) acc[k] = 0;
+  constexpr int V = 4;
+  for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {""", """  uint32_t acc[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) acc[k] = 0;
+  constexpr int V = 4;
+  if (bstart && (s1 - s0) * NB > 4 * bstart[NB]) plain = 0;  // a run 4x the mean: a hub's
+  for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {""")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }
