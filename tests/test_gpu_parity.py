@@ -408,6 +408,29 @@ def test_evaluate_rejects_missing_part(api):
     assert e.value.code == -34  # -ERANGE
 
 
+def test_degree_64k_id_buckets_repeatable(api, options):
+    """The 64K-id histogram on a skewed power law (41.6 M ids, 2^28 records, hub degrees in the
+    hundreds of thousands): three passes give identical degrees summing to 2m - self-loops
+    (LLAMA). Guards the LDS-draining barriers: with a barrier compiled without the wait, late
+    LDS adds of one wave were lost or moved run to run."""
+    import torch
+    from sheep_amd import capi, device
+
+    options(degree=2)
+    n_ids, m = 41652230, 1 << 28
+    uv = device.powerlaw(n_ids, m, 2.1, 50.0, 5, 0, m)
+    u = uv.view(torch.int32)
+    loops = int((u[:, 0] == u[:, 1]).sum())
+    ref = None
+    for _ in range(3):
+        d = device.degree(uv, n_ids, capi.DEGREE_LLAMA).view(torch.int32).to(torch.int64)
+        assert int(d.sum()) == 2 * m - loops
+        if ref is None:
+            ref = d
+        else:
+            assert torch.equal(d, ref)
+
+
 @pytest.mark.parametrize("hist", ["1", "0"])
 def test_degree_64k_id_buckets(oracle, api, options, hist):
     """Id spaces above 2^25 use buckets of 65536 ids: the one-read histogram with u16 LDS
