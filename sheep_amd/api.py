@@ -12,6 +12,7 @@ Names and argument meaning follow arpang/sheep lib/:
 Errors raise SheepError (the reference throws / asserts: see include/sheep_amd.h).
 """
 import ctypes
+import errno
 
 import numpy as np
 
@@ -205,8 +206,16 @@ def mpi_sequence(uv, n_ids=0, mode=DEGREE_LLAMA):
     cap = max(int(n_ids), int(uv.max()) + 1 if uv.size else 0, 1)
     seq = np.zeros(cap, np.uint32)
     n = ctypes.c_uint32(0)
-    capi.call("sheep_mpi_sequence", _ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
-              ctypes.byref(n))
+    rc = capi.lib().sheep_mpi_sequence(_ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
+                                       ctypes.byref(n))
+    if rc == -errno.ERANGE and n.value > cap:
+        # this rank's ids do not span the sequence: every rank got -ERANGE with the global
+        # length (the smallest buffer of all ranks decides), so all retry together
+        cap = n.value
+        seq = np.zeros(cap, np.uint32)
+        rc = capi.lib().sheep_mpi_sequence(_ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
+                                           ctypes.byref(n))
+    capi.check(rc, "sheep_mpi_sequence")
     return seq[:n.value]
 
 

@@ -115,13 +115,16 @@ def lib():
     return L
 
 
+def check(r, name):
+    """Raise SheepError for a negative ABI return r of function `name`."""
+    if r < 0:
+        raise SheepError(r, "%s: %s" % (name, lib().sheep_last_error().decode()))
+    return r
+
+
 def call(name, *args):
     """Invoke an ABI function; raise SheepError on a negative return."""
-    L = lib()
-    r = getattr(L, name)(*args)
-    if r < 0:
-        raise SheepError(r, "%s: %s" % (name, L.sheep_last_error().decode()))
-    return r
+    return check(getattr(lib(), name)(*args), name)
 
 
 def last_timings():

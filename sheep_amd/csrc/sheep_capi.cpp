@@ -1688,6 +1688,8 @@ static uint32_t ingest_dat(Ctx& c, FILE* f, uint64_t lo, uint64_t m, uint32_t* d
     HIP_CHECK(hipMemcpyAsync(c.h_pinned, dmax, 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     mx = c.h_pinned[0];
+    if (mx == INV)  // max id + 1 does not fit u32: a record names INVALID (or 0xFFFFFFFE)
+      throw ApiError(-ERANGE, "a record's vertex id is 0xFFFFFFFE or 0xFFFFFFFF (u32 id space)");
   } catch (...) {
     cleanup();
     throw;
@@ -1752,9 +1754,11 @@ int sheep_partition_edges(const uint32_t* edges_uv, uint64_t m, const int16_t* p
   API_BEGIN
   Ctx& c = ctx();
   hipStream_t s = c.stream;
-  uint32_t n_ids = n_parts_vid;
-  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
-  for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
+  uint64_t top = n_parts_vid;  // 64-bit: an id 0xFFFFFFFF would wrap max id + 1 to 0
+  for (uint64_t i = 0; i < 2 * m; ++i) top = std::max<uint64_t>(top, (uint64_t)edges_uv[i] + 1);
+  for (uint32_t i = 0; i < n_seq; ++i) top = std::max<uint64_t>(top, (uint64_t)seq[i] + 1);
+  if (top > 0xFFFFFFFEull) throw ApiError(-ERANGE, "partition_edges: vertex id 0xFFFFFFFF (INVALID)");
+  const uint32_t n_ids = (uint32_t)top;
   uint32_t* uv = upload_records(c, edges_uv, m, s);
   int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
   HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));
@@ -1946,15 +1950,22 @@ int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int
   hipStream_t s = c.stream;
   if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
     throw ApiError(-EINVAL, "degree_mode");
-  // MPI_Allreduce MAX of the id spaces (sequence.h:72), then SUM of the degrees (:78)
-  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
-  int64_t* d_n = (int64_t*)c.scratch.get("mt_cnt", 8);
-  int64_t hn = n_ids;
-  HIP_CHECK(hipMemcpyAsync(d_n, &hn, 8, hipMemcpyHostToDevice, s));
-  comm.allreduce_max_i64(d_n, 1, s);
-  HIP_CHECK(hipMemcpyAsync(&hn, d_n, 8, hipMemcpyDeviceToHost, s));
+  // MPI_Allreduce MAX of the id spaces (sequence.h:72), then SUM of the degrees (:78).  The
+  // smallest seq_cap of all ranks travels with it (as -cap under MAX), so that a sequence longer
+  // than some rank's buffer fails on EVERY rank after the same collectives (n_seq is the same
+  // everywhere): no rank leaves the others waiting in a later collective.
+  uint64_t top = n_ids;  // 64-bit: an id 0xFFFFFFFF would wrap max id + 1 to 0
+  for (uint64_t i = 0; i < 2 * m; ++i) top = std::max<uint64_t>(top, (uint64_t)edges_uv[i] + 1);
+  int64_t* d_n = (int64_t*)c.scratch.get("mt_cnt", 16);
+  int64_t hn[2] = {(int64_t)top, -(int64_t)seq_cap};
+  HIP_CHECK(hipMemcpyAsync(d_n, hn, 16, hipMemcpyHostToDevice, s));
+  comm.allreduce_max_i64(d_n, 2, s);
+  HIP_CHECK(hipMemcpyAsync(hn, d_n, 16, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  n_ids = (uint32_t)hn;
+  if (hn[0] > (int64_t)0xFFFFFFFFll)
+    throw ApiError(-ERANGE, "mpi_sequence: vertex id 0xFFFFFFFF (INVALID) in the records");
+  n_ids = (uint32_t)hn[0];
+  const uint64_t min_cap = (uint64_t)(-hn[1]);
   uint32_t* uv = upload_records(c, edges_uv, m, s);
   const size_t n = std::max<uint32_t>(n_ids, 1);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", n * 4);
@@ -1965,7 +1976,8 @@ int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int
   comm.allreduce_sum_u32(deg, n_ids, s);
   uint32_t n_seq = sequence_dev(c, deg, n_ids, seq, rank, s);
   if (n_seq_out) *n_seq_out = n_seq;
-  if (n_seq > seq_cap) throw ApiError(-ERANGE, "mpi_sequence: seq_out holds fewer ids than the sequence");
+  if (n_seq > min_cap)  // on every rank at once (see above); the caller grows seq_out and retries
+    throw ApiError(-ERANGE, "mpi_sequence: a rank's seq_out holds fewer ids than the sequence");
   if (n_seq) HIP_CHECK(hipMemcpyAsync(seq_out, seq, (size_t)n_seq * 4, hipMemcpyDeviceToHost, s));
   check_err(c, s);
   API_END
@@ -2103,8 +2115,12 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
   hipStream_t s = c.stream;
   if (degree_mode != SHEEP_DEGREE_LLAMA && degree_mode != SHEEP_DEGREE_FILE)
     throw ApiError(-EINVAL, "degree_mode");
-  if (n_ids == 0)
-    for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
+  if (n_ids == 0) {
+    uint64_t top = 0;  // 64-bit: an id 0xFFFFFFFF would wrap max id + 1 to 0
+    for (uint64_t i = 0; i < 2 * m; ++i) top = std::max<uint64_t>(top, (uint64_t)edges_uv[i] + 1);
+    if (top > 0xFFFFFFFEull) throw ApiError(-ERANGE, "degree_seq: vertex id 0xFFFFFFFF (INVALID)");
+    n_ids = (uint32_t)top;
+  }
   uint32_t* uv = upload_records(c, edges_uv, m, s);
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)n_ids * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("rank", (size_t)n_ids * 4);
@@ -2125,9 +2141,11 @@ int sheep_evaluate(const uint32_t* edges_uv, uint64_t m, const int16_t* parts, u
   API_BEGIN
   Ctx& c = ctx();
   hipStream_t s = c.stream;
-  uint32_t n_ids = n_parts_vid;
-  for (uint64_t i = 0; i < 2 * m; ++i) n_ids = std::max(n_ids, edges_uv[i] + 1);
-  for (uint32_t i = 0; i < n_seq; ++i) n_ids = std::max(n_ids, seq[i] + 1);
+  uint64_t top = n_parts_vid;  // 64-bit: an id 0xFFFFFFFF would wrap max id + 1 to 0
+  for (uint64_t i = 0; i < 2 * m; ++i) top = std::max<uint64_t>(top, (uint64_t)edges_uv[i] + 1);
+  for (uint32_t i = 0; i < n_seq; ++i) top = std::max<uint64_t>(top, (uint64_t)seq[i] + 1);
+  if (top > 0xFFFFFFFEull) throw ApiError(-ERANGE, "evaluate: vertex id 0xFFFFFFFF (INVALID)");
+  const uint32_t n_ids = (uint32_t)top;
   uint32_t* uv = upload_records(c, edges_uv, m, s);
   int16_t* dparts = (int16_t*)c.scratch.get("h_parts", (size_t)std::max<uint32_t>(n_ids, 1) * 2);
   HIP_CHECK(hipMemsetAsync(dparts, 0xFF, (size_t)n_ids * 2, s));  // INVALID_PART = -1

@@ -2897,7 +2897,8 @@ __global__ void k_strip_xs1(const uint32_t* __restrict__ raw, uint64_t n, uint32
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t t = raw[3 * i], h = raw[3 * i + 1];
     ((uint2*)uv)[i] = make_uint2(t, h);
-    mx = max(mx, max(t, h) + 1);
+    const uint32_t top = max(t, h);  // an id 0xFFFFFFFF (INVALID) saturates: the host rejects it
+    mx = max(mx, top == INV ? INV : top + 1);
   }
   for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
   if ((threadIdx.x & 63) == 0 && mx) atomicMax(max_id, mx);

@@ -4,11 +4,19 @@
 // reference's scripts hand results between workers (write a .tmp, then rename it).
 //   torchrun --no-python --nproc-per-node N graph2tree G -ir ...   (RANK, WORLD_SIZE, LOCAL_RANK)
 //   mpirun -n N graph2tree G -ir ...          (OMPI_COMM_WORLD_RANK / _SIZE / _LOCAL_RANK)
-// SHEEP_COMM_DIR (default /tmp) holds the id file; its name comes from SHEEP_COMM_KEY, else the
-// launcher's job (TORCHELASTIC_RUN_ID, MASTER_PORT, OMPI_MCA_ess_base_jobid).
+// SHEEP_COMM_DIR (default /tmp) holds the id file.  Its name joins every job-identifying variable
+// the launcher set (SHEEP_COMM_KEY, TORCHELASTIC_RUN_ID, MASTER_ADDR, MASTER_PORT,
+// OMPI_MCA_ess_base_jobid): a plain torchrun has run id "none", and MASTER_ADDR:MASTER_PORT is
+// what keeps two jobs on one host apart.  Rank 0 removes a file left under that name before it
+// writes the new one and on every error path; the other ranks ignore a file written more than
+// kStaleSec before they started (a crashed run's).
 #pragma once
+#include <sys/stat.h>
 #include <unistd.h>
 
+#include <ctime>
+
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -46,29 +54,40 @@ struct ProcessGroup {
     const std::string path = id_path();
     uint8_t id[SHEEP_COMM_ID_BYTES];
     if (rank == 0) {
-      sheep_check(sheep_comm_unique_id(id), "comm id");
+      unlink(path.c_str());  // a crashed run's id must not be read by this job's ranks
       const std::string tmp = path + ".tmp";
-      FILE* f = fopen(tmp.c_str(), "wb");
-      if (!f || fwrite(id, 1, sizeof id, f) != sizeof id || fclose(f) != 0)
-        throw std::runtime_error("cannot write " + tmp);
-      if (rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
+      try {
+        sheep_check(sheep_comm_unique_id(id), "comm id");
+        FILE* f = fopen(tmp.c_str(), "wb");
+        if (!f || fwrite(id, 1, sizeof id, f) != sizeof id || fclose(f) != 0)
+          throw std::runtime_error("cannot write " + tmp);
+        if (rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
+        sheep_check(sheep_comm_init(id, size, rank), "comm init");  // collective
+      } catch (...) {
+        unlink(tmp.c_str());
+        unlink(path.c_str());
+        throw;
+      }
+      unlink(path.c_str());
     } else {
+      const time_t started = time(nullptr);
       auto until = std::chrono::steady_clock::now() + std::chrono::seconds(120);
       for (;;) {
+        struct stat st;
         FILE* f = fopen(path.c_str(), "rb");
         if (f) {
+          const bool fresh = fstat(fileno(f), &st) == 0 && st.st_mtime + kStaleSec >= started;
           size_t got = fread(id, 1, sizeof id, f);
           fclose(f);
-          if (got == sizeof id) break;
+          if (fresh && got == sizeof id) break;
         }
         if (std::chrono::steady_clock::now() > until)
           throw std::runtime_error("rank " + std::to_string(rank) + ": no communicator id at " + path);
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
       }
+      sheep_check(sheep_comm_init(id, size, rank), "comm init");  // collective: all ranks joined
     }
-    sheep_check(sheep_comm_init(id, size, rank), "comm init");  // collective: all ranks joined
     joined = true;
-    if (rank == 0) unlink(path.c_str());
   }
 
   ~ProcessGroup() {
@@ -76,13 +95,17 @@ struct ProcessGroup {
   }
 
  private:
+  static constexpr long kStaleSec = 60;  // ranks start within a minute of each other
+
   static std::string id_path() {
     const char* dir = getenv("SHEEP_COMM_DIR");
     std::string key;
-    for (const char* k : {"SHEEP_COMM_KEY", "TORCHELASTIC_RUN_ID", "MASTER_PORT", "OMPI_MCA_ess_base_jobid"})
-      if (getenv(k)) {
-        key = getenv(k);
-        break;
+    for (const char* k : {"SHEEP_COMM_KEY", "TORCHELASTIC_RUN_ID", "MASTER_ADDR", "MASTER_PORT",
+                          "OMPI_MCA_ess_base_jobid"})
+      if (const char* v = getenv(k)) {
+        if (!key.empty()) key += '-';
+        for (const char* p = v; *p; ++p)  // a file name: keep [A-Za-z0-9._]
+          key += (isalnum((unsigned char)*p) || *p == '.' || *p == '_') ? *p : '_';
       }
     if (key.empty()) key = "default";
     return std::string(dir ? dir : "/tmp") + "/sheep-comm-" + key + ".id";

@@ -35,15 +35,22 @@ std::vector<vid_t> degreeSequence(GraphType const& graph) {
 
 // mpiSequence (sequence.h:65-93): this rank's partial graph; the id spaces MAX-reduced and the
 // degrees SUM-reduced over the ranks (RCCL; a ProcessGroup from comm.h must be joined), so
-// every rank gets the same sequence.
+// every rank gets the same sequence.  getMaxVid() is this rank's share only (its records), and
+// the global sequence can be longer: then EVERY rank gets -ERANGE with the global length
+// (sheep_mpi_sequence compares with the smallest buffer of all ranks), and all retry together.
 template <typename GraphType>
 std::vector<vid_t> mpiSequence(GraphType const& graph) {
   graph.to_device();
   std::vector<vid_t> seq(std::max<vid_t>(graph.getMaxVid(), 1));
   uint32_t n_seq = 0;
-  sheep_check(sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
-                                 SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq),
-              "mpiSequence");
+  int rc = sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
+                              SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq);
+  if (rc == -ERANGE && n_seq > seq.size()) {
+    seq.resize(n_seq);
+    rc = sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
+                            SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq);
+  }
+  sheep_check(rc, "mpiSequence");
   seq.resize(n_seq);
   return seq;
 }

@@ -5,6 +5,8 @@ RCCL refuses two ranks on one device, so the P-rank driver is run as P threads o
 on cuda:0 (sheep_graph2tree_multi_local: the same C++ loop, its collectives as device copies),
 and the RCCL communicator itself over a one-rank group (the code path of every rank of the
 8-GPU run, collectives included)."""
+import errno
+
 import numpy as np
 import pytest
 
@@ -80,6 +82,17 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
         check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
         seq = api.mpi_sequence(hep_edges, int(hep_edges.max()) + 1)
         assert np.array_equal(seq, oracle.degree_sequence(hep_edges))
+        # a rank whose buffer is shorter than the global sequence (its share spans few ids):
+        # -ERANGE with the global length, after the collectives; the retry then succeeds
+        import ctypes
+        from sheep_amd import capi
+        small = np.zeros(4, np.uint32)
+        n = ctypes.c_uint32(0)
+        rc = capi.lib().sheep_mpi_sequence(api._ptr(hep_edges), hep_edges.shape[0], 0, 0,
+                                           api._ptr(small), 4, ctypes.byref(n))
+        assert rc == -errno.ERANGE and n.value == seq.size
+        assert np.array_equal(api.mpi_sequence(hep_edges[:100]),
+                              oracle.degree_sequence(hep_edges[:100]))
         t = api.build_tree_multi(hep_edges, seq)
         p, w = oracle.build_tree(hep_edges, seq)
         assert np.array_equal(t.parent, p) and np.array_equal(t.pst, w)
@@ -106,3 +119,25 @@ def test_multi_local_front_half_options(oracle, gpu, options, env):
     torch.cuda.synchronize()
     out = device.graph2tree_multi_local(shards_of(uv_d, 2), 1 << 19)
     check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
+
+
+def test_multi_local_one_rank_overflows(oracle, gpu):
+    """Only one rank's direct bins overflow (its shard holds the records with the highest hi,
+    far beyond its share of the global estimate): that rank groups its records through the
+    scatter while the other stays direct; the tree is still the serial one."""
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.rmat(19, 16, 14)
+    torch.cuda.synchronize()
+    uv = uv_d.cpu().numpy().view(np.uint32)
+    seq = oracle.degree_sequence(uv)
+    rk = np.full(1 << 19, 0xFFFFFFFF, np.uint64)
+    rk[seq] = np.arange(seq.size)
+    hi = np.maximum(rk[uv[:, 0]], rk[uv[:, 1]])
+    order = np.argsort(-hi.astype(np.int64), kind="stable")
+    cut = uv.shape[0] // 10  # rank 0: the 10 % of records with the highest hi
+    a = torch.from_numpy(np.ascontiguousarray(uv[order[:cut]]).view(np.int32)).cuda()
+    b = torch.from_numpy(np.ascontiguousarray(uv[order[cut:]]).view(np.int32)).cuda()
+    out = device.graph2tree_multi_local([a.view(torch.uint32), b.view(torch.uint32)], 1 << 19)
+    check(oracle, uv, 0, *out)
