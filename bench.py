@@ -45,8 +45,10 @@ def pmc_traffic(kernel, key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         tab = json.load(open(path))[key]
+        base, _, targ = kernel.partition("<")  # "k_part<1>" matches "k_part<1, 512, 16>"
         for k, rec in tab.items():
-            if k.replace("sheep::", "").split("<")[0] == kernel:
+            kb, _, kt = k.replace("sheep::", "").partition("<")
+            if kb == base and (not targ or kt.split(",")[0].rstrip(">").strip() == targ.rstrip(">")):
                 return rec["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         pass
@@ -204,33 +206,44 @@ def main():
         ms_per_step = 1e3 * elapsed / args.steps
         n_seq = out[3] if world > 1 else out[3]
         value = m / (elapsed / args.steps)
-        # Roofline of the dominant kernel: the one with the most time per step among those
-        # bracketed live by HIP events on the stream they run on:
-        #   k_kb_map (one launch per bucket, side stream): 8 B per record streamed + 4 B per
-        #     rank of hi counts; its union-find / label gathers are not algorithmic bytes;
-        #   k_edge_bin (one launch, the direct-binning edge pass over k_part's (x, rank y)
-        #     records): 8 B record read + 4 B rank word gathered + 8 B item written.
+        # Roofline of the dominant kernel: the one with the most time per step among the
+        # kernels bracketed live by HIP events on the stream they run on.
+        # "algo" is SURVEY §8(d)'s compulsory bytes attributed to the kernel: the degree pass's
+        # one read of the records (k_fh_count), the degree writes (the histogram), the rank/tree
+        # pass's one read of the records plus the hi counts (k_kb_map); regrouping passes and
+        # rank gathers count zero there.  "io" is the kernel's own streaming bytes (reads of its
+        # input, writes of its output, 4 B per gathered rank), reported beside it.
         avg = {k: sum(v) / len(v) for k, v in phase.items()}
         recs = hi - lo if world > 1 else m
         key = "rmat%d" % scale if args.workload == "rmat" else args.workload
+        # (kernel, phase, launches-phase or None, algo bytes per step, io bytes per step)
+        table = [("k_kb_map", "kb_map", "kb_map#", 8 * recs + 4 * n_seq, 8 * recs + 4 * n_seq),
+                 ("k_edge_bin", "edge_pass", None, 0, 20 * recs),
+                 ("k_part<1>", "partition", None, 0, 20 * recs),
+                 ("k_fh_scatter", "degree_scatter", None, 0, 20 * recs),
+                 ("k_fh_count", "degree_count", None, 8 * recs, 8 * recs),
+                 ("k_degb_hist16", "degree_hist", None, 4 * n_ids, 4 * recs + 4 * n_ids)]
         cands = []
-        if "edge_pass" in avg:
-            cands.append(("k_edge_bin", avg["edge_pass"], 1, 20 * recs))
-        if avg.get("kb_map#"):
-            cands.append(("k_kb_map", avg["kb_map"], avg["kb_map#"], 8 * recs + 4 * n_seq))
+        for name, ph, nph, algo, io in table:
+            if avg.get(ph):
+                launches = avg[nph] if nph else 1
+                if launches:
+                    cands.append((name, avg[ph], launches, algo, io))
         roof = None
         if cands:
-            name, ms, launches, algo = max(cands, key=lambda c: c[1])
+            name, ms, launches, algo, io = max(cands, key=lambda c: c[1])
             per_launch_ms = ms / launches
             ach = (algo / launches) / (per_launch_ms * 1e-3)
             roof = {"kernel": name, "bound": "hbm", "achieved": ach / 1e9,
                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
                     "traffic": pmc_traffic(name, key), "algo_bytes": algo / launches,
+                    "io_bytes": io / launches, "io_GB_s": io / (ms * 1e-3) / 1e9,
                     "avg_ms": per_launch_ms, "launches_per_step": launches,
                     "ms_per_step": ms,
                     "phases_ms": {k: round(v, 3) for k, v in avg.items() if not k.endswith("#")},
                     "others": {c[0]: {"ms_per_step": round(c[1], 3),
-                                      "GB_s": round(c[3] / (c[1] * 1e-3) / 1e9, 1),
+                                      "algo_GB_s": round(c[3] / (c[1] * 1e-3) / 1e9, 1),
+                                      "io_GB_s": round(c[4] / (c[1] * 1e-3) / 1e9, 1),
                                       "traffic_per_launch": pmc_traffic(c[0], key)}
                                for c in cands if c[0] != name}}
         # SURVEY §8d B(m, n) = 16 m + 24 n with n = the id slots (its C4 row: 18.79 GB); the ids

@@ -18,9 +18,11 @@
  * Types follow lib/defs.h:76-82: ids, jnids and weights are uint32, INVALID = 0xFFFFFFFF.
  * An edge stream is m records of (tail, head) as 2*m uint32 (the XS1 weight is dropped).
  *
- * Size limits (offsets and counters are u32): a tree build takes m < 2^32 records, a degree
- * pass (2m endpoints) m < 2^31, the partition evaluation 2m < 2^32 adjacency entries; larger
- * inputs return -EINVAL.  Shard them (-l n/k + merge, or the multi-GPU entry points).
+ * Size limits: every call takes m < 2^32 records (record offsets and counters are u32; larger
+ * inputs return -EINVAL: shard them with -l n/k + merge, or the multi-GPU entry points).  The
+ * degree pass counts endpoints with record offsets beyond 2^31 records (the fused pass of
+ * graph2tree); the partition evaluation sorts at most 2^31 adjacency entries per pass and
+ * beyond that walks id ranges, so only a single vertex with more than 2^31 entries is refused.
  */
 #ifndef SHEEP_AMD_H
 #define SHEEP_AMD_H
@@ -44,7 +46,9 @@ extern "C" {
 /* ---- device / library ------------------------------------------------------------------- */
 
 /* Select the HIP device for this thread's calls and create the library stream + scratch.
- * Replaces the process/device setup around MPI_Init in graph2tree.cpp:134-157. */
+ * Replaces the process/device setup around MPI_Init in graph2tree.cpp:134-157.  It takes the
+ * device INDEX, not SURVEY §8b's draft n_devices: one process (MPI rank) drives one GPU, so
+ * a rank names its own device (LOCAL_RANK); the multi-GPU calls below take the rank count. */
 int sheep_gpu_init(int device);
 
 /* ---- records resident in HBM (the graph LLAMA keeps in RAM, graph_wrapper.h:43-63) --------
@@ -79,9 +83,8 @@ int sheep_abi_version(void);
  * variables, read ONCE when the library first initialises a device; afterwards only these
  * calls change them (process-wide).  Names: degree, edge_part, part_overlap, seq_compact,
  * sort, kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, kb_defer, degb_plain, degb_hist, bin_tm,
- * bin_scatter, ep_plain, tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum.  -EINVAL for an
- * unknown
- * name. */
+ * bin_scatter, ep_plain, tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum, eval_pass.
+ * -EINVAL for an unknown name. */
 int sheep_set_option(const char* name, long long value);
 int sheep_get_option(const char* name, long long* value);
 
@@ -100,7 +103,11 @@ int sheep_degree_seq(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int d
  * jtree.cpp:112-145 -> insert jtree.cpp:65-110).  parent_out/pst_out hold n_seq entries.
  * Errors: -EINVAL if seq repeats an id (the reference asserts, jtree.h:166);
  *         -ERANGE if an edge joins a seq vertex to an id > max(seq) (index.at throws,
- *         jtree.cpp:75). */
+ *         jtree.cpp:75).
+ * No n_ids argument (SURVEY §8b's draft had one): the reference sizes its rank index by
+ * max(seq) + 1 (jtree.h:113-122), and that bound, not the id space, decides which records are
+ * ignored and which raise index.at's out_of_range; a separate n_ids could only disagree with
+ * it.  The device entry points below take n_ids because there the caller owns the rank map. */
 int sheep_build_tree(const uint32_t* edges_uv, uint64_t m, const uint32_t* seq, uint32_t n_seq,
                      uint32_t* parent_out, uint32_t* pst_out);
 

@@ -7,8 +7,11 @@ The product is ``libsheep_amd.so`` (HIP kernels for gfx950 behind the C-ABI decl
 * :mod:`sheep_amd.api`      — the reference's lib/ interface in Python: ``degree_sequence``,
   ``file_sequence``, ``JTree``/``build_tree``, ``JNodeTable.merge``, ``Facts``,
   ``Partition``/``evaluate`` and the .dat/.net/.tre/.seq formats.
-* :mod:`sheep_amd.dist`     — the sharded multi-GPU pipeline (one process per GPU,
-  torch.distributed over RCCL): degree all-reduce + log2(P) partial-tree merge.
+* :mod:`sheep_amd.device`   — the device-pointer calls on torch tensors, including the
+  multi-GPU driver (``graph2tree_multi``: one process per GPU over the library's own RCCL
+  communicator — degree all-reduce, then one kb bucket loop walked by all ranks).
+* :mod:`sheep_amd.dist`     — the same multi-rank loop orchestrated from Python over
+  torch.distributed (the gloo rehearsal), and the per-rank partial trees merged on rank 0.
 
 There is no CPU fallback: if the HIP library cannot be loaded every compute call raises.
 """

@@ -48,7 +48,7 @@ static const KnobDef kKnobs[] = {
     {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
-    {"kb_gsum", &Knobs::kb_gsum},
+    {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
 };
 
 static Knobs g_knobs;
@@ -241,8 +241,18 @@ struct Timer {
 // Read and clear the device error word (synchronises s).
 static void check_err(Ctx& c, hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(c.h_pinned, c.d_err, 4, hipMemcpyDeviceToHost, s));
+  uint32_t* fw = fault_word();  // the device's walk guard (sheep_kernels.hip)
+  if (fw) HIP_CHECK(hipMemcpyAsync(c.h_pinned + 12, fw, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   uint32_t e = c.h_pinned[0];
+  if (fw && c.h_pinned[12]) {
+    const uint32_t f = c.h_pinned[12];
+    HIP_CHECK(hipMemsetAsync(fw, 0, 4, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    throw ApiError(-EIO, std::string("device walk guard tripped (") +
+                             ((f & 1) ? "forest not heap-ordered" : "union-find cycle") +
+                             "): corrupt intermediate data");
+  }
   if (e) {
     HIP_CHECK(hipMemsetAsync(c.d_err, 0, 4, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -292,7 +302,20 @@ static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
     if (stats) launch_deg_stats(d_deg, n_ids, stats, s);
     return false;
   }
-  require_endpoints(m, "degree");
+  if (2 * m >= (1ull << 32) && fh_tmp_words(m, n_ids) > 1) {
+    // beyond the endpoint array's u32 offsets: the fused pass, whose offsets count records
+    // (it also writes the records grouped by y bucket, into scratch here)
+    require_records(m, "degree");
+    uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", fh_tmp_words(m, n_ids) * 4);
+    uint64_t* recs = (uint64_t*)c.scratch.get("e_items", m * 8);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* st = stats ? stats : (uint32_t*)c.scratch.get("stats", 16);
+    launch_fh_front(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, recs, pws, st, s);
+    if (counted) HIP_CHECK(hipEventRecord(counted, s));
+    return false;
+  }
+  // (ids beyond 2^26: launch_degree_bucketed takes the global-atomic pass, no offsets)
+  if (degb_tmp_words(m, n_ids, nullptr, nullptr) > 1) require_endpoints(m, "degree");
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
   uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
   return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist,
@@ -1501,12 +1524,25 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   // pass and the sequence sort (SHEEP_PART_OVERLAP=0: in line, after them; =1: after the
   // whole degree pass).
   const int ov = knobs().part_overlap;
-  const bool overlap = ov != 0 && m > 0 && use_part(m);
-  if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
-  const bool yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
-                             overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
-  tm.mark("degree");
+  // Fused (ov 3): the degree pass itself writes the records grouped by y bucket
+  // (launch_fh_front), so the first partition pass and its read are gone.
+  bool fused = false;
+  if (ov == 3 && use_part(m) && knobs().degree != 1 && fh_tmp_words(m, n_ids) > 1) {
+    require_records(m, "degree");  // its offsets count records, not endpoints
+    uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", fh_tmp_words(m, n_ids) * 4);
+    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    fused = launch_fh_front(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, mid, pws,
+                            stats, s, [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
+  }
+  const bool overlap = !fused && ov != 0 && m > 0 && use_part(m);
+  if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
+  const bool yh = fused ? false
+                        : degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
+                                     overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
+  tm.mark(fused ? "degree_hist" : "degree");
+  if (fused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
@@ -1517,10 +1553,13 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   }
   uint32_t* nsd = (uint32_t*)c.scratch.get("nsd", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
   uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true, nsd, selfc, degree_mode);
+  // an id out of range leaves the fused pass's record array short: report it before the
+  // partition passes read the array (the stream is idle here: sequence_dev synchronised it)
+  if (fused) check_err(c, s);
   tm.mark("sequence");
   DegInfo di;
   di.nsd = nsd;
-  di.part_first_done = overlap;
+  di.part_first_done = overlap || fused;
   di.yhist_ready = yh;
   di.seq = d_seq;
   di.deg = deg;
@@ -1538,15 +1577,43 @@ static void evaluate_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const int16_t
                          const uint32_t* d_rank, uint32_t n_ids, uint32_t n_parts, uint64_t* out,
                          hipStream_t s) {
   if (n_parts == 0 || n_parts > 32768) throw ApiError(-EINVAL, "n_parts must be in [1, 32768]");
-  if (2 * m >= (1ull << 32)) throw ApiError(-EINVAL, "evaluate: 2m adjacency entries must fit u32");
   uint32_t* deg = (uint32_t*)c.scratch.get("deg", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
   launch_degree(d_uv, m, n_ids, SHEEP_DEGREE_LLAMA, deg, nullptr, c.d_err, s);
-  uint64_t* keys = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(2 * m, 1) * 8);
-  uint64_t* keys_b = (uint64_t*)c.scratch.get("e_items_b", std::max<uint64_t>(2 * m, 1) * 8);
-  uint32_t* rtmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(2 * m) * 4);
+  // Each metric sorts one key per adjacency entry (2m of them, less the self-loops' second).
+  // Beyond 2^eval_pass entries the ids are cut into ranges whose entries (their LLAMA degrees)
+  // fit a pass, and each pass sorts only the entries of its range.
+  const int ep = std::min(31, std::max(10, knobs().eval_pass));
+  std::vector<std::pair<uint32_t, uint64_t>> passes;
+  uint64_t n_keys = 2 * m;
+  if (2 * m > (1ull << ep)) {
+    check_err(c, s);  // an id out of range would leave the degrees short
+    std::vector<uint32_t> hdeg(n_ids);
+    if (n_ids) HIP_CHECK(hipMemcpyAsync(hdeg.data(), deg, (size_t)n_ids * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    const uint64_t cap = 1ull << ep;
+    uint64_t run = 0;
+    n_keys = 0;
+    passes.emplace_back(0u, 0ull);
+    for (uint32_t v = 0; v < n_ids; ++v) {
+      if (hdeg[v] > cap) throw ApiError(-EINVAL, "evaluate: one vertex has more adjacency entries than a pass");
+      if (run + hdeg[v] > cap) {
+        passes.back().second = run;
+        n_keys = std::max(n_keys, run);
+        passes.emplace_back(v, 0ull);
+        run = 0;
+      }
+      run += hdeg[v];
+    }
+    passes.back().second = run;
+    n_keys = std::max(n_keys, run);
+  }
+  uint64_t* keys = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(n_keys, 1) * 8);
+  uint64_t* keys_b = (uint64_t*)c.scratch.get("e_items_b", std::max<uint64_t>(n_keys, 1) * 8);
+  uint32_t* rtmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(std::max<uint64_t>(n_keys, 1)) * 4);
   const size_t wsn = 4 * (size_t)n_parts + 8;
   unsigned long long* ws = (unsigned long long*)c.scratch.get("eval_ws", wsn * 8);
-  launch_evaluate(d_uv, m, d_parts, d_rank, deg, n_ids, n_parts, keys, keys_b, rtmp, ws, c.d_err, s);
+  launch_evaluate(d_uv, m, d_parts, d_rank, deg, n_ids, n_parts, keys, keys_b, rtmp, ws, c.d_err, s,
+                  &passes);
   std::vector<unsigned long long> h(wsn);
   HIP_CHECK(hipMemcpyAsync(h.data(), ws, wsn * 8, hipMemcpyDeviceToHost, s));
   check_err(c, s);  // synchronises; -ERANGE for an id, part or position out of range

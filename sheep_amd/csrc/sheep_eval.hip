@@ -76,6 +76,41 @@ __global__ void k_ev_keys(const uint2* __restrict__ uv, uint64_t m, const int16_
   }
 }
 
+// The keys of the entries X -> Y with X in [v0, v1) only (a pass of an evaluation whose 2m
+// entries exceed one sort), appended in any order at keys[*n_out ...] (wave-aggregated); the
+// caller filled keys with ~0 up to the pass's bound.  Distinct keys of different passes differ
+// in X, so the passes' distinct counts add up.
+template <int METRIC>
+__global__ void k_ev_keys_range(const uint2* __restrict__ uv, uint64_t m,
+                                const int16_t* __restrict__ parts, const uint32_t* __restrict__ pos,
+                                uint32_t v0, uint32_t v1, uint64_t* __restrict__ keys,
+                                unsigned long long* n_out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x; b < m; b += stride) {  // wave-uniform
+    const uint64_t e = b + threadIdx.x;
+    uint64_t k0 = ~0ull, k1 = ~0ull;
+    if (e < m) {
+      const uint2 r = uv[e];
+      if (r.x >= v0 && r.x < v1) k0 = ev_key<METRIC>(r.x, r.y, parts, pos);
+      if (r.x != r.y && r.y >= v0 && r.y < v1) k1 = ev_key<METRIC>(r.y, r.x, parts, pos);
+    }
+    const uint32_t c = (k0 != ~0ull) + (k1 != ~0ull);
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
+    }
+    const uint32_t tot = __shfl(inc, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && tot) base = atomicAdd(n_out, (unsigned long long)tot);
+    base = __shfl(base, 63);
+    uint64_t at = base + inc - c;
+    if (k0 != ~0ull) keys[at++] = k0;
+    if (k1 != ~0ull) keys[at] = k1;
+  }
+}
+
 // Number of distinct keys (~0 excluded) of a sorted array.
 __global__ void k_ev_distinct(const uint64_t* __restrict__ keys, uint64_t n,
                               unsigned long long* out) {
@@ -173,7 +208,7 @@ __global__ void k_ev_nodes(const uint32_t* __restrict__ deg, uint32_t n_ids,
 void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const uint32_t* pos,
                      const uint32_t* deg, uint32_t n_ids, uint32_t k, uint64_t* keys,
                      uint64_t* keys_b, uint32_t* rtmp, unsigned long long* ws, uint32_t* err,
-                     hipStream_t s) {
+                     hipStream_t s, const std::vector<std::pair<uint32_t, uint64_t>>* passes) {
   unsigned long long* hist = ws;             // [0, 3k): hash, down, up balances
   unsigned long long* vbal = ws + 3 * k;     // [3k, 4k)
   unsigned long long* cnt = ws + 4 * (uint64_t)k;  // cut, self, nodes, vcom, hash, down, up
@@ -186,6 +221,30 @@ void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const
   for (uint32_t v = n_ids ? n_ids - 1 : 0; v; v >>= 1) ++idb;
   // one more bit than the values need in each sort: a ~0 sentinel (missing second entry of a
   // self-loop, a Vcom entry inside X's own part) then sorts after every real key
+  if (passes && !passes->empty()) {
+    // passes: (first id, keys bound) of consecutive id ranges, the last one ending at n_ids
+    unsigned long long* nk = cnt + 7;
+    for (int metric = 0; metric < 4; ++metric)
+      for (size_t p = 0; p < passes->size(); ++p) {
+        const uint32_t v0 = (*passes)[p].first;
+        const uint32_t v1 = p + 1 < passes->size() ? (*passes)[p + 1].first : n_ids;
+        const uint64_t n = std::max<uint64_t>((*passes)[p].second, 1);
+        auto kk = metric == EV_VCOM ? k_ev_keys_range<EV_VCOM>
+                : metric == EV_HASH ? k_ev_keys_range<EV_HASH>
+                : metric == EV_DOWN ? k_ev_keys_range<EV_DOWN> : k_ev_keys_range<EV_UP>;
+        (void)hipMemsetAsync(keys, 0xFF, n * 8, s);
+        (void)hipMemsetAsync(nk, 0, 8, s);
+        hipLaunchKernelGGL(kk, dim3(ev_grid(m)), dim3(EV_BLOCK), 0, s, (const uint2*)uv, m, parts,
+                           pos, v0, v1, keys, nk);
+        uint64_t* by_part = radix_sort_u64(keys, keys_b, keys, n, 0, 16, rtmp, s);
+        uint64_t* other = by_part == keys ? keys_b : keys;
+        hipLaunchKernelGGL(k_ev_swap, dim3(ev_grid(n)), dim3(EV_BLOCK), 0, s, by_part, n);
+        const uint64_t* sorted = radix_sort_u64(by_part, other, by_part, n, 0, idb + 1, rtmp, s);
+        hipLaunchKernelGGL(k_ev_distinct, dim3(ev_grid(n)), dim3(EV_BLOCK), 0, s, sorted, n,
+                           cnt + 3 + metric);
+      }
+    return;
+  }
   const uint64_t n = 2 * m;
   for (int metric = 0; metric < 4; ++metric) {
     auto kk = metric == EV_VCOM ? k_ev_keys<EV_VCOM>

@@ -16,6 +16,10 @@ constexpr uint32_t INV = 0xFFFFFFFFu;
 constexpr uint32_t ERR_RANGE = 1u;      // an id >= n_ids, or index.at(nbr) out of range
 constexpr uint32_t ERR_DUP_SEQ = 2u;    // an id repeated in seq
 
+// The current device's walk-guard word (sheep_kernels.hip): non-zero after a zipper or
+// union-find walk met corrupt data and stopped; check_err reports it as -EIO and clears it.
+uint32_t* fault_word();
+
 // Growable device scratch.  One instance per device; slots are named so that the hot path
 // reuses its buffers across calls (allocation only happens on the first / a larger call).
 struct Scratch {
@@ -33,8 +37,9 @@ struct Scratch {
 struct Knobs {
   int degree = 0;        // SHEEP_DEGREE: 0 auto (bucketed from 2^18 records), 1 atomic, 2 bucketed
   int edge_part = -1;    // SHEEP_EDGE_PART: partitioned rank gathers; -1 auto (m >= 2^22), 0, 1
-  int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
-                         //   after it (1), in line (0)
+  int part_overlap = 3;  // SHEEP_PART_OVERLAP: first partition pass fused into the degree
+                         //   scatter (3, graph2tree_dev), beside the degree pass (2), after it
+                         //   (1), in line (0)
   int seq_compact = 1;   // SHEEP_SEQ_COMPACT: sort only the ids with degree > 0
   int sort_radix = 0;    // SHEEP_SORT (1 = "radix"): two radix passes instead of the hi bins
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
@@ -56,6 +61,8 @@ struct Knobs {
   int kb_gsum = -1;      // SHEEP_KB_GSUM: the map tests 64-rank "all in the giant" blocks in LDS
                          //   first; -1 auto (from 2^27 records), 0, 1
   int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
+  int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
+                         //   of the partition evaluation (more: passes over id ranges)
 };
 Knobs& knobs();  // the process-wide options (sheep_capi.cpp)
 
@@ -100,6 +107,16 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                             hipStream_t s, uint32_t* yhist = nullptr,
                             hipEvent_t counted = nullptr /* recorded once yhist is complete */,
                             uint32_t* stats = nullptr /* [0] max degree, [1] zero-degree ids */);
+// Fused front half (graph2tree_dev): degrees (deg, selfc, stats as launch_degree_bucketed)
+// and the records (x, y) grouped by y bucket into recs (m u64), the x digits of
+// launch_part_second counted into part_ws[256, 512) — what launch_part_first produced.  tmp:
+// fh_tmp_words (1: not applicable, n_ids beyond 2^26).  False when not applicable.
+size_t fh_tmp_words(uint64_t m, uint32_t n_ids);
+bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
+                     uint32_t* selfc, uint32_t* err, uint32_t* tmp, uint64_t* recs,
+                     uint32_t* part_ws, uint32_t* stats, hipStream_t s,
+                     void (*mark)(void*, const char*) = nullptr /* phase marks (timing) */,
+                     void* mark_arg = nullptr);
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats /*[0]=max,[1]=zeros*/,
                       hipStream_t s);
 // Exclusive scan of n u32 (n < 2^32); tmp needs scan_tmp_words(n) u32.
@@ -236,10 +253,14 @@ void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hi
 // Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)
 // vertex balance, then cut, self-loop records, nodes, and the distinct keys of vcom, hash,
 // down, up.  keys/keys_b: 2m u64; rtmp: rsort_tmp_words(2m) u32; deg: LLAMA degrees.
+// passes (nullable / empty: one pass over the 2m entries): (first id, keys bound) of
+// consecutive id ranges; each pass sorts only the entries X -> Y with X in its range (keys /
+// keys_b then need the largest bound, not 2m).  ws[4k + 7] is the passes' append counter.
 void launch_evaluate(const uint32_t* uv, uint64_t m, const int16_t* parts, const uint32_t* pos,
                      const uint32_t* deg, uint32_t n_ids, uint32_t k, uint64_t* keys,
                      uint64_t* keys_b, uint32_t* rtmp, unsigned long long* ws, uint32_t* err,
-                     hipStream_t s);
+                     hipStream_t s,
+                     const std::vector<std::pair<uint32_t, uint64_t>>* passes = nullptr);
 // graph2tree -p K -o OUT (sheep_eval.hip): the non-self-loop records as (min, max) pairs,
 // grouped by the part of their lower-sequence endpoint, each part in (min, record) order.
 // items / items_b: m u64; rtmp: rsort_tmp_words(m); out: 2m u32; pstart: n_parts + 1 u64.

@@ -44,6 +44,22 @@ static unsigned device_cus() {
   return cached;
 }
 
+// Device fault word.  The tree kernels trust what earlier kernels wrote (ranks, offsets, the
+// forest), and a corrupt input could turn a walk into an endless loop (a lab variant that left
+// the degree scatter's output unwritten once hung a later kernel).  So every unbounded walk is
+// guarded: a zipper walk that meets a parent not above its child, or a union-find walk longer
+// than FAULT_STEPS, stops and raises the fault; the host reports it as -EIO after the call.
+__device__ uint32_t g_fault;
+static constexpr uint32_t FAULT_STEPS = 1u << 26;
+__device__ __forceinline__ void raise_fault(uint32_t bit) { atomicOr(&g_fault, bit); }
+constexpr uint32_t FAULT_FOREST = 1u, FAULT_UF = 2u;
+
+uint32_t* fault_word() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fault)) != hipSuccess) return nullptr;
+  return (uint32_t*)p;
+}
+
 static inline unsigned grid_for(uint64_t n, int per_block = BLOCK) {
   uint64_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -295,6 +311,11 @@ void launch_scan_exclusive(const uint32_t* in, uint32_t* out, uint64_t n, uint32
 // Supports n_ids <= 2^26 (launch_degree_bucketed falls back to k_degree above that).
 // ---------------------------------------------------------------------------------------
 static constexpr int DEGB_THREADS = 1024;
+// A record streamed once (non-temporal: it should not evict what the other kernels keep).
+__device__ __forceinline__ uint2 ld_rec_nt(const uint2* p) {
+  const uint64_t v = __builtin_nontemporal_load((const uint64_t*)p);
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
 // k_deg_stats folded into the histogram kernels: the block's max degree and zero-degree ids,
 // two global atomics per block (called by every thread of a DEGB_THREADS block).
 __device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, uint32_t zeros) {
@@ -419,19 +440,42 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
             uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
-            uint32_t* __restrict__ stats, int plain) {
+            uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
+            const unsigned long long* __restrict__ bstart2 = nullptr,
+            const uint64_t* __restrict__ rec0 = nullptr) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) cnt[i] = 0;
   block_sync();
+  const int lane = threadIdx.x & 63;
+  // ep2 (nullable, tile-major bstart2): a second endpoint array (the fused front half's x ids)
+  for (int sg = 0; sg < (ep2 ? 2 : 1); ++sg) {
+  const uint16_t* __restrict__ ep_s = sg ? ep2 : ep;
   // bstart (tile-major counts): bucket starts and the total; else the digit-major offsets
   const uint64_t last = (uint64_t)NB * nchunks - 1;
-  uint64_t s0 = bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
-  uint64_t s1 = bstart ? bstart[b + 1]
-                       : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
-                                      : (uint64_t)offsets[last] + counts[last];
-  const int lane = threadIdx.x & 63;
+  uint64_t s0 = sg ? bstart2[b] : bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
+  uint64_t s1 = sg ? bstart2[b + 1]
+                   : bstart ? bstart[b + 1]
+                            : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                           : (uint64_t)offsets[last] + counts[last];
+  if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
+    const uint32_t lm = (1u << SH) - 1u;
+    for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
+      uint2 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * DEGB_THREADS + threadIdx.x;
+        q[u] = i < s1 ? ld_rec_nt((const uint2*)rec0 + i) : make_uint2(0, INV);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t e = q[u].y & lm;
+        if (q[u].y != INV && (H == 1 || (e >> 15) == h)) atomicAdd(&cnt[H > 1 ? (e & (DEGB_HALF - 1)) : e], 1u);
+      }
+    }
+    continue;
+  }
   // 32 entries (four 16-B loads, all issued before use: the loop is latency-bound otherwise)
   // per thread per iteration, from the 8-aligned entry below s0 (ep is padded: the loads may
   // run up to 7 entries past the end)
@@ -441,7 +485,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
-      q[u] = i < s1 ? *(const uint4*)(ep + i) : make_uint4(0, 0, 0, 0);
+      q[u] = i < s1 ? *(const uint4*)(ep_s + i) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < V; ++u) {
@@ -470,6 +514,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
       }
     }
   }
+  }  // segments
   block_sync();
   uint64_t g0 = ((uint64_t)b << SH) + (uint64_t)h * span;
   uint32_t mx = 0, zeros = 0;
@@ -492,29 +537,51 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
               const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, uint32_t n_ids,
               uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
-              uint32_t* __restrict__ stats, int plain) {
+              uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
+              const unsigned long long* __restrict__ bstart2 = nullptr,
+              const uint64_t* __restrict__ rec0 = nullptr) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const uint64_t last = (uint64_t)NB * nchunks - 1;
-  const uint64_t s0 = bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
-  const uint64_t s1 = bstart ? bstart[b + 1]
-                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
-                                            : (uint64_t)offsets[last] + counts[last];
   uint32_t acc[64];
 #pragma unroll
   for (int k = 0; k < 64; ++k) acc[k] = 0;
   constexpr int V = 4;
+  // ep2 (nullable, tile-major bstart2): a second endpoint array (the fused front half's x ids)
+  for (int sg = 0; sg < (ep2 ? 2 : 1); ++sg) {
+  const uint16_t* __restrict__ ep_s = sg ? ep2 : ep;
+  const uint64_t last = (uint64_t)NB * nchunks - 1;
+  const uint64_t s0 = sg ? bstart2[b] : bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
+  const uint64_t s1 = sg ? bstart2[b + 1]
+                         : bstart ? bstart[b + 1]
+                                  : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                                 : (uint64_t)offsets[last] + counts[last];
   for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
     const uint64_t g1 = min(g0 + 65535, s1);
     for (uint32_t i = threadIdx.x; i < 32768; i += DEGB_THREADS) pk[i] = 0;
     block_sync();
+    if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
+      for (uint64_t i0 = g0; i0 < g1; i0 += 8 * DEGB_THREADS) {
+        uint2 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint64_t i = i0 + (uint64_t)u * DEGB_THREADS + threadIdx.x;
+          q[u] = i < g1 ? ld_rec_nt((const uint2*)rec0 + i) : make_uint2(0, INV);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (q[u].y != INV) {
+            const uint32_t v = q[u].y & 0xFFFFu;
+            atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
+          }
+      }
+    } else
     for (uint64_t i0 = g0 & ~7ull; i0 < g1; i0 += 8 * V * DEGB_THREADS) {
       uint4 q[V];
 #pragma unroll
       for (int u = 0; u < V; ++u) {
         uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
-        q[u] = i < g1 ? *(const uint4*)(ep + i) : make_uint4(0, 0, 0, 0);
+        q[u] = i < g1 ? *(const uint4*)(ep_s + i) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < V; ++u) {
@@ -550,6 +617,7 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
     }
     block_sync();
   }
+  }  // segments
   const uint64_t base = (uint64_t)b << 16;
   uint32_t mx = 0, zeros = 0;
 #pragma unroll
@@ -660,6 +728,228 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
                        deg, (const unsigned long long*)bstart, stats, degb_plain() >> 1);
   return yhist != nullptr;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused front half (graph2tree_dev, large inputs): the degree pass also performs the first
+// partition of the rank gathers.  One counting read and one scattering read of the records:
+//   k_fh_count    per 32K-record chunk: records per y bucket (2^SH ids), x endpoints per x
+//                 bucket (LLAMA: x != y only; a self-loop counts once), and the x digits of the
+//                 second partition pass (global, 256 counters) -> two tile-major count rows
+//   k_fh_scatter  LDS counting sorts: the chunk's x ids (u16) by x bucket, and in four
+//                 8K-record parts the RECORDS by y bucket
+//   k_degb_hist16 / k_degb_hist  one workgroup per bucket over its records' y ids, then its
+//                 x ids.
+// The records come out grouped by y bucket — what the first pass of launch_part_gather
+// produced from a second read — so the second pass (k_part<1>) gathers rank[y] from 256 KB
+// slices.  Bytes per record: 8 (count) + 8 + 8 + 2 (scatter) + 8 + 2 (histogram) = 36,
+// against 8 + 12 + 4 for the degree pass and 16 for the partition pass before.
+// Chunks are dealt to blocks XCD-contiguously (xcd_chunk): the blocks of one XCD scatter
+// consecutive chunks, whose runs of a bucket are adjacent in memory, so the short runs of the
+// u16 arrays merge into whole lines in that XCD's L2.
+// ---------------------------------------------------------------------------------------
+
+
+// Block b -> chunk: blocks b and b + 8 share an XCD (round-robin dispatch; for speed only), so
+// each group of blocks b % 8 takes one contiguous range of the n chunks (a bijection).
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n) {
+  const uint32_t q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_fh_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
+           uint32_t NB, uint32_t* __restrict__ cy, uint32_t* __restrict__ cx, uint32_t* err,
+           int psh, uint32_t* __restrict__ xdig) {
+  __shared__ uint32_t hy[DEGB_NB], hx[DEGB_NB], xd[256];
+  for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) { hy[i] = 0; hx[i] = 0; }
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) xd[i] = 0;
+  block_sync();
+  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
+  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
+  constexpr int U = 8;
+  for (int r = 0; r < DEGB_CHUNK / (DEGB_THREADS * U); ++r) {
+    uint2 e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + threadIdx.x;
+      e[u] = i < cn ? ld_rec_nt(uv + base + i) : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t i = (uint32_t)(r * U + u) * DEGB_THREADS + threadIdx.x;
+      if (i >= cn) continue;
+      if (e[u].x >= n_ids || e[u].y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
+      atomicAdd(&hy[e[u].y >> SH], 1u);
+      if (file_mode || e[u].x != e[u].y) atomicAdd(&hx[e[u].x >> SH], 1u);
+      atomicAdd(&xd[part_digit(e[u].x, psh)], 1u);
+    }
+  }
+  block_sync();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+    if (xd[i]) atomicAdd(&xdig[i], xd[i]);
+  for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) {
+    cy[(uint64_t)blockIdx.x * NB + i] = hy[i];
+    cx[(uint64_t)blockIdx.x * NB + i] = hx[i];
+  }
+}
+
+// The chunk's x ids are staged whole (64 KB of u16, one run per x bucket as in k_degb_scatter:
+// ~64-B runs) — staged per part, their 16-B runs would each cost a 64-B HBM write (measured:
+// 26.5 GB written for 12.9 GB of data).  The records go out per 8K-record part (64-B runs).
+// The y ids are not written separately: the histogram reads them from the records.
+static constexpr int FH_PART = 8192, FH_PARTS = DEGB_CHUNK / FH_PART;
+
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_fh_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
+             uint32_t NB, const uint32_t* __restrict__ cx, const uint32_t* __restrict__ offy,
+             const uint32_t* __restrict__ offx, uint64_t* __restrict__ recs,
+             uint16_t* __restrict__ epx, uint32_t* __restrict__ selfc) {
+  __shared__ uint16_t xbuf[DEGB_CHUNK];  // 64 KB: the chunk's x ids by x bucket
+  __shared__ uint64_t stage[FH_PART];    // 64 KB: a part's records by y bucket
+  __shared__ uint32_t sy[DEGB_NB + 1], xs[DEGB_NB], xcur[DEGB_NB], goy[DEGB_NB], gox[DEGB_NB];
+  __shared__ uint32_t wsum[DEGB_THREADS / 64];
+  constexpr int IT = FH_PART / DEGB_THREADS;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t lmask = (1u << SH) - 1u;
+  const uint32_t c = xcd_chunk(blockIdx.x, gridDim.x);
+  // the chunk's x runs: exclusive scan of its x count row (k_fh_count)
+  {
+    const uint32_t v = t < (int)NB ? cx[(uint64_t)c * NB + t] : 0u;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    if (t < (int)NB) {
+      goy[t] = offy[(uint64_t)c * NB + t];
+      gox[t] = offx[(uint64_t)c * NB + t];
+    }
+    block_sync();
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    if (t < (int)NB) { xs[t] = add + inc - v; xcur[t] = add + inc - v; }
+  }
+  const uint64_t base = (uint64_t)c * DEGB_CHUNK;
+  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
+  uint2 e[IT], en[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const uint32_t j = (uint32_t)(k * DEGB_THREADS + t);
+    e[k] = j < cn ? ld_rec_nt(uv + base + j) : make_uint2(INV, INV);
+  }
+  for (int h = 0; h < FH_PARTS; ++h) {
+    if (t < (int)NB) sy[t] = 0;
+    block_sync();
+    uint32_t ky[IT];  // rank inside the part's y run (INV: not stored)
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      ky[k] = INV;
+      if (e[k].x >= n_ids || e[k].y >= n_ids) continue;  // padding, or ERR_RANGE (k_fh_count)
+      const bool loop = e[k].x == e[k].y;
+      ky[k] = atomicAdd(&sy[e[k].y >> SH], 1u);
+      if (file_mode || !loop) xbuf[atomicAdd(&xcur[e[k].x >> SH], 1u)] = (uint16_t)(e[k].x & lmask);
+      if (loop && selfc) atomicAdd(&selfc[e[k].x], 1u);
+    }
+    block_sync();
+    const uint32_t v = t < (int)NB ? sy[t] : 0u;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    block_sync();
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    if (t < (int)NB) sy[t] = add + inc - v;
+    if (t == DEGB_THREADS - 1) sy[NB] = add + inc;
+    block_sync();
+#pragma unroll
+    for (int k = 0; k < IT; ++k)
+      if (ky[k] != INV) stage[sy[e[k].y >> SH] + ky[k]] = ((uint64_t)e[k].y << 32) | e[k].x;
+    if (h + 1 < FH_PARTS) {  // the next part's records, in flight during this part's writes
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const uint32_t j = (uint32_t)((h + 1) * FH_PART + k * DEGB_THREADS + t);
+        en[k] = j < cn ? ld_rec_nt(uv + base + j) : make_uint2(INV, INV);
+      }
+    }
+    block_sync();
+    // written flat: thread j stores staged record j at its run's position (full waves even
+    // where the runs are short; a run continues the previous part's, chunk after chunk)
+    const uint32_t ny = sy[NB];
+    for (uint32_t j = t; j < ny; j += DEGB_THREADS) {
+      const uint64_t r = stage[j];
+      const uint32_t b = (uint32_t)(r >> 32) >> SH;
+      recs[(uint64_t)goy[b] + (j - sy[b])] = r;
+    }
+    block_sync();
+    if (t < (int)NB) goy[t] += sy[t + 1] - sy[t];  // the next part continues each run
+#pragma unroll
+    for (int k = 0; k < IT; ++k) e[k] = en[k];
+  }
+  block_sync();
+  // each wave writes whole x runs
+  for (uint32_t b = w; b < NB; b += DEGB_THREADS / 64) {
+    const uint32_t s0 = xs[b], n = xcur[b] - s0, g = gox[b];
+    for (uint32_t j = lane; j < n; j += 64) epx[(uint64_t)g + j] = xbuf[s0 + j];
+  }
+}
+
+// Scratch of launch_fh_front (u32 words): two count and two offset matrices, the tile-major
+// scan's group sums and bucket starts for each, and the u16 x id array (16-B aligned, padded).
+size_t fh_tmp_words(uint64_t m, uint32_t n_ids) {
+  int SH = 0;
+  uint32_t NB = 0;
+  if (!degb_params(n_ids, &SH, &NB)) return 1;
+  const uint64_t nchunks = (m + DEGB_CHUNK - 1) / DEGB_CHUNK;
+  const uint64_t cw = (uint64_t)NB * nchunks;
+  const uint64_t gw = (uint64_t)NB * ((nchunks + TM_G - 1) / TM_G);
+  return 4 * cw + 2 * (gw + 2 * (NB + 1) + 8) + (m + 16) / 2 + 16;
+}
+
+bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
+                     uint32_t* selfc, uint32_t* err, uint32_t* tmp, uint64_t* recs,
+                     uint32_t* part_ws, uint32_t* stats, hipStream_t s,
+                     void (*mark)(void*, const char*), void* mark_arg) {
+  int SH;
+  uint32_t NB;
+  if (m == 0 || n_ids == 0 || !degb_params(n_ids, &SH, &NB)) return false;
+  if (SH > 15 && !knobs().degb_hist16) return false;
+  const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
+  const uint64_t cw = (uint64_t)NB * nchunks;
+  const uint64_t gw = (uint64_t)NB * ((nchunks + TM_G - 1) / TM_G);
+  uint32_t* cy = tmp;
+  uint32_t* cx = cy + cw;
+  uint32_t* oy = cx + cw;
+  uint32_t* ox = oy + cw;
+  auto align8 = [](uint32_t* p) { return (uint32_t*)(((uintptr_t)p + 7) & ~(uintptr_t)7); };
+  uint32_t* gy = ox + cw;
+  unsigned long long* by = (unsigned long long*)align8(gy + gw);
+  uint32_t* gx = (uint32_t*)(by + NB + 2);
+  unsigned long long* bx = (unsigned long long*)align8(gx + gw);
+  auto align16 = [](void* p) { return (uint16_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15); };
+  uint16_t* epx = align16(bx + NB + 2);
+  if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  (void)hipMemsetAsync(part_ws, 0, 512 * 4, s);  // [256, 512): the x digits of k_part<1>
+  int pbits = 0;
+  for (uint32_t v = n_ids - 1; v; v >>= 1) ++pbits;
+  const int psh = pbits > 8 ? pbits - 8 : 0;  // as launch_part_gather with n_rank = n_ids
+  hipLaunchKernelGGL(k_fh_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
+                     n_ids, file_mode, SH, NB, cy, cx, err, psh, part_ws + 256);
+  tm_offsets(cy, oy, nchunks, NB, NB, gy, by, s);
+  tm_offsets(cx, ox, nchunks, NB, NB, gx, bx, s);
+  if (mark) mark(mark_arg, "degree_count");
+  hipLaunchKernelGGL(k_fh_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
+                     n_ids, file_mode, SH, NB, (const uint32_t*)cx, (const uint32_t*)oy,
+                     (const uint32_t*)ox, recs, epx, selfc);
+  if (mark) mark(mark_arg, "degree_scatter");
+  if (SH > 15)
+    hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)nullptr,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, n_ids, deg,
+                       (const unsigned long long*)by, stats, degb_plain() & 1,
+                       (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
+  else
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)nullptr,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, SH, 1u,
+                       n_ids, deg, (const unsigned long long*)by, stats, degb_plain() >> 1,
+                       (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1820,6 +2110,10 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
   }
   s.fresh = false;
   if (s.p < s.b) {  // INVALID is never < b
+    if (s.p <= s.x) {  // not heap-ordered: corrupt input; stop the walk (fault_word)
+      raise_fault(FAULT_FOREST);
+      return true;
+    }
     if (JUMP && s.prev != INV) jump[s.prev] = s.p;
     s.prev = s.x;
     s.x = s.p;
@@ -2008,13 +2302,18 @@ __device__ __forceinline__ uint32_t uf_prio(uint32_t x) {  // a bijection on u32
 }
 
 // find with path halving.  ATOMIC: loads with relaxed agent atomics (during concurrent unions).
+// (A walk longer than FAULT_STEPS means a cycle — corrupt input: it stops at x, fault_word.)
 template <bool ATOMIC>
 __device__ __forceinline__ uint32_t uf_find(uint32_t* uf, uint32_t x) {
-  for (;;) {
+  for (uint32_t k = 0;; ++k) {
     uint32_t p = ATOMIC ? __hip_atomic_load(&uf[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : uf[x];
     if (p == x) return x;
     uint32_t gp = ATOMIC ? __hip_atomic_load(&uf[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : uf[p];
     if (gp == p) return p;
+    if (k == FAULT_STEPS) {
+      raise_fault(FAULT_UF);
+      return x;
+    }
     uf[x] = gp;  // x is a non-root forever; any ancestor is a valid pointer
     x = gp;
   }
@@ -2023,19 +2322,28 @@ __device__ __forceinline__ uint32_t uf_find(uint32_t* uf, uint32_t x) {
 // find without path compression, for values every thread of a launch asks for (G): a
 // compressing find would have all of them write the same words.
 __device__ __forceinline__ uint32_t uf_find_ro(const uint32_t* uf, uint32_t x) {
-  for (uint32_t p = uf[x]; p != x; p = uf[x]) x = p;
+  uint32_t k = 0;
+  for (uint32_t p = uf[x]; p != x; p = uf[x]) {
+    if (++k == FAULT_STEPS) {
+      raise_fault(FAULT_UF);
+      break;
+    }
+    x = p;
+  }
   return x;
 }
 
 // Link order: R (the giant's root, see k_kb_union) above everything, then uf_prio — a strict
-// total order, so concurrent links never close a cycle.
+// total order, so concurrent links never close a cycle.  Each retry follows a link another
+// thread made; more than FAULT_STEPS of them (or a find that gave up) means corrupt input.
 __device__ __forceinline__ void uf_union(uint32_t* uf, uint32_t u, uint32_t v, uint32_t R) {
-  for (;;) {
+  for (uint32_t k = 0; k < FAULT_STEPS; ++k) {
     uint32_t ru = uf_find<true>(uf, u), rv = uf_find<true>(uf, v);
     if (ru == rv) return;
     if (ru == R || (rv != R && uf_prio(ru) > uf_prio(rv))) { uint32_t t = ru; ru = rv; rv = t; }
     if (atomicCAS(&uf[ru], ru, rv) == ru) return;
   }
+  raise_fault(FAULT_UF);
 }
 
 // The kb map pass over one bucket's records (sorted by hi down to groups of 2^gshift ranks,

@@ -34,11 +34,12 @@ class JTree {
   JTree(GraphType const& graph, std::vector<vid_t> const& seq, Options opts = Options()) {
     build(graph, seq, opts);
   }
+  // built into a mapped .tre (jtree.h:125-137: the table is the file, jnode.cpp:52-74)
   template <typename GraphType>
   JTree(GraphType const& graph, std::vector<vid_t> const& seq, char const* filename,
-        Options opts = Options()) {
+        Options opts = Options())
+      : jnodes(filename, (jnid_t)seq.size()) {
     build(graph, seq, opts);
-    jnodes.save(filename);
   }
   // graph2tree -i -r in one collective step (ranks of a joined ProcessGroup, comm.h): the tree
   // of the union of every rank's partial graph under the shared seq, on every rank — the
@@ -56,10 +57,10 @@ class JTree {
       sheep_check(sheep_build_tree_multi(graph.records_data(), graph.records(), seq.data(),
                                          (uint32_t)seq.size(), parent.data(), pst.data()),
                   "JTree (collective)");
-    jnodes = JNodeTable(parent, pst);
+    jnodes.assign(parent, pst);
   }
 
-  // open constructor (jtree.h:138-143)
+  // open constructor (jtree.h:138-143): the .tre mapped in place
   JTree(std::vector<vid_t> const& seq, char const* filename) : jnodes(filename) { make_index(seq); }
 
   jnid_t vid2jnid(vid_t X) const { return X < index.size() ? index[X] : INVALID_JNID; }
@@ -119,6 +120,6 @@ class JTree {
       sheep_check(sheep_build_tree(graph.records_data(), graph.records(), seq.data(),
                                    (uint32_t)seq.size(), parent.data(), pst.data()),
                   "JTree");
-    jnodes = JNodeTable(parent, pst);
+    jnodes.assign(parent, pst);
   }
 };

@@ -101,3 +101,43 @@ def test_fullsize_8_ranks(gpu, name):
     del shards
     torch.cuda.empty_cache()
     gpu.call("sheep_release")
+
+
+@pytest.mark.gpu
+def test_rmat27_beyond_u32_endpoints(gpu):
+    """R-MAT scale 27: 2^31 records, 2^32 endpoints — past round 2's u32 endpoint offsets (the
+    fused degree pass counts records, so one GPU takes m < 2^32).  Checked without a CPU run,
+    by properties that hold at any size:
+      * the whole stream's degrees equal the sum of its two halves' (each half on the bucketed
+        endpoint path, within the old limits);
+      * the whole stream's tree equals the exact merge of the two halves' trees, each built on
+        the global seq (etree(G1 ∪ G2) = etree(etree(G1) ∪ etree(G2)); pst summed: the merge of
+        jnode.cpp:174-201, what graph2tree -l + merge_trees relies on, README:112-121)."""
+    import torch
+
+    from sheep_amd import device
+
+    scale, n_ids = 27, 1 << 27
+    uv = device.rmat(scale, 16, 27)
+    m = uv.shape[0]
+    assert 2 * m == 1 << 32
+    seq, parent, pst, n = device.graph2tree(uv, n_ids)
+    deg, _ = device.degree_ex(uv, n_ids)
+    h = m // 2
+    d0, s0 = device.degree_ex(uv[:h], n_ids)
+    d1, s1 = device.degree_ex(uv[h:], n_ids)
+    torch.cuda.synchronize()
+    i32 = lambda t: t.view(torch.int32)  # noqa: E731 (u32 add = i32 add, two's complement)
+    assert torch.equal(i32(deg), i32(d0) + i32(d1))
+    seq2, rank, n2 = device.sequence(deg)
+    assert n2 == n and torch.equal(i32(seq2[:n]), i32(seq[:n]))
+    pa, wa = device.build_tree_deg(uv[:h], rank, seq2, n, d0, s0)
+    pb, wb = device.build_tree_deg(uv[h:], rank, seq2, n, d1, s1)
+    device.merge_into(pa, wa, pb, wb, n)
+    torch.cuda.synchronize()
+    assert torch.equal(i32(pa[:n]), i32(parent[:n]))
+    assert torch.equal(i32(wa[:n]), i32(pst[:n]))
+    # and the forest is heap-ordered (parent > child, INVALID at the roots)
+    p = parent[:n].to(torch.int64) & 0xFFFFFFFF
+    idx = torch.arange(n, device=p.device)
+    assert bool(((p == 0xFFFFFFFF) | (p > idx)).all())

@@ -92,6 +92,8 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
     (18, 29, 0, {"bin_scatter": 0, "bin_direct": 0}),  # stable bin scatter
+    (18, 30, 0, {"part_overlap": 2}),  # unfused: the first partition pass beside the degrees
+    (18, 31, 1, {"part_overlap": 0}),  # unfused, in line
 ])
 def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
@@ -112,6 +114,27 @@ def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env)
     assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
     assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+@pytest.mark.parametrize("n,m,mode", [((1 << 26) + 5, (1 << 22) + 12345, 0),
+                                      ((1 << 25) + 77, (1 << 22) + 1, 1)])
+def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, n, m, mode):
+    """The fused front half (launch_fh_front) with 64K-id buckets (n_ids > 2^25: the one-read
+    u16 histogram over the y ids then the x ids) and a ragged last chunk: seq, parent and pst
+    bit-exact in both degree conventions."""
+    import torch
+    from sheep_amd import device
+
+    uv_d = device.powerlaw(n, m, 2.2, 80.0, 9 + mode)
+    uv = uv_d.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    seq = oracle.degree_sequence(uv, mode)
+    s_d, p_d, w_d, k = device.graph2tree(uv_d, n, mode)
+    torch.cuda.synchronize()
+    p, w = oracle.build_tree(uv, seq)
+    assert k == len(seq)
+    assert np.array_equal(s_d[:k].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:k].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
 
 
 @pytest.mark.parametrize("n,m,gamma,i0,seed", [(1000, 20000, 2.3, 100.0, 3),
@@ -183,6 +206,22 @@ def test_neighbour_beyond_seq_is_erange(api):
     with pytest.raises(api.SheepError) as e:
         api.build_tree(uv, np.array([0, 1], np.uint32))
     assert e.value.code == -34
+
+
+def test_corrupt_forest_trips_walk_guard(oracle, api):
+    """A tree that is not heap-ordered (parent[1] = 0 < 1) would send the zipper's walk in a
+    circle; the walk guard stops it and the call fails with -EIO (fault_word), after which the
+    device works normally again (the guard word is cleared)."""
+    inv = 0xFFFFFFFF
+    a = api.JNodeTable(np.array([2, 0, inv], np.uint32), np.zeros(3, np.uint32))
+    b = api.JNodeTable(np.array([1, inv, inv], np.uint32), np.zeros(3, np.uint32))
+    with pytest.raises(api.SheepError) as e:
+        api.merge_trees(a, b)
+    assert e.value.code == -5
+    good = api.JNodeTable(np.array([2, 2, inv], np.uint32), np.zeros(3, np.uint32))
+    g = api.merge_trees(good, b)
+    p, s = oracle.merge(good.parent, good.pst, b.parent, b.pst)
+    assert np.array_equal(g.parent, p) and np.array_equal(g.pst, s)
 
 
 def test_empty_and_isolated(oracle, api):
@@ -384,6 +423,16 @@ def test_evaluate_rmat_matches_checker(oracle, api, scale, k):
     """R-MAT streams carry self-loops and duplicate records: both adjacency conventions of the
     evaluation (a self-loop is one entry; duplicates count) are exercised."""
     uv = oracle.rmat(scale, 16, 70 + scale)
+    got, want = _eval_case(oracle, uv, k, scale)
+    assert got == want
+
+
+@pytest.mark.parametrize("scale,k,ep", [(14, 16, 16), (16, 64, 18)])
+def test_evaluate_in_id_range_passes(oracle, api, options, scale, k, ep):
+    """The evaluation's id-range passes (taken beyond 2^31 adjacency entries, e.g. a 2^31-record
+    graph), forced here at 2^ep entries per pass: every number equals the checker's."""
+    options(eval_pass=ep)
+    uv = oracle.rmat(scale, 16, 90 + scale)
     got, want = _eval_case(oracle, uv, k, scale)
     assert got == want
 
