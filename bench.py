@@ -55,6 +55,19 @@ def pmc_traffic(kernel, key):
     return None
 
 
+def host_cpus():
+    """The host's logical CPUs, those this process may run on, and its cgroup CPU quota."""
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    return {"logical": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "quota": quota,
+            "model": cpu_model()}
+
+
 def cpu_baseline(scale, edgefactor, seed):
     """Single-thread CPU restatement of graph2tree's Sorted+Mapped window (oracle, the
     reference's algorithm with FastUnionFind) on a bounded sample: R-MAT `scale`."""
@@ -220,6 +233,7 @@ def main():
         table = [("k_kb_map", "kb_map", "kb_map#", 8 * recs + 4 * n_seq, 8 * recs + 4 * n_seq),
                  ("k_edge_bin", "edge_pass", None, 0, 20 * recs),
                  ("k_part<1>", "partition", None, 0, 20 * recs),
+                 ("k_part<0>", "part_first", "part_first#", 0, 16 * recs),
                  ("k_fh_scatter", "degree_scatter", None, 0, 20 * recs),
                  ("k_fh_count", "degree_count", None, 8 * recs, 8 * recs),
                  ("k_degb_hist16", "degree_hist", None, 4 * n_ids, 4 * recs + 4 * n_ids)]
@@ -269,9 +283,13 @@ def main():
                                       args.workload)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef, args.cpu_scale)
-            # the box's CPU share (the harness sets OMP_NUM_THREADS to it); nproc shows more
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
+            # `mpirun -n <cores>`: the cores this job may use — its cgroup CPU quota (the GPU
+            # box: cpu.max 1600000/100000 = 16 of the host's 256 logical CPUs); more ranks than
+            # that only time-slice inside the quota
+            cpus = host_cpus()
+            threads = cpus["quota"] or cpus["affinity"]
             rec["cpu_baseline_ir"] = cpu_baseline_ir(args.cpu_scale, ef, args.cpu_scale, threads)
+            rec["cpu_baseline_ir"]["host_cpus"] = cpus
         print(json.dumps(rec), flush=True)
     if native:
         device.comm_free()

@@ -1525,10 +1525,13 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   // whole degree pass).
   const int ov = knobs().part_overlap;
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
-  // Fused (ov 3): the degree pass itself writes the records grouped by y bucket
-  // (launch_fh_front), so the first partition pass and its read are gone.
+  // Fused (ov 3, and always past 2^31 records, where the endpoint offsets of the unfused
+  // degree pass end): the degree pass itself writes the records grouped by y bucket
+  // (launch_fh_front), so the first partition pass and its read are gone.  Not the default:
+  // it moves fewer bytes but in shorter runs, and measured no faster.
   bool fused = false;
-  if (ov == 3 && use_part(m) && knobs().degree != 1 && fh_tmp_words(m, n_ids) > 1) {
+  if ((ov == 3 || 2 * m >= (1ull << 32)) && use_part(m) && knobs().degree != 1 &&
+      fh_tmp_words(m, n_ids) > 1) {
     require_records(m, "degree");  // its offsets count records, not endpoints
     uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", fh_tmp_words(m, n_ids) * 4);
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
@@ -1548,7 +1551,9 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
     if (ov != 2) HIP_CHECK(hipEventRecord(c.part_ev[0], s));
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
+    const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench
     launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
+    tm.span_end(sp, c.side);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
   uint32_t* nsd = (uint32_t*)c.scratch.get("nsd", (size_t)std::max<uint32_t>(n_ids, 1) * 4);

@@ -37,9 +37,9 @@ struct Scratch {
 struct Knobs {
   int degree = 0;        // SHEEP_DEGREE: 0 auto (bucketed from 2^18 records), 1 atomic, 2 bucketed
   int edge_part = -1;    // SHEEP_EDGE_PART: partitioned rank gathers; -1 auto (m >= 2^22), 0, 1
-  int part_overlap = 3;  // SHEEP_PART_OVERLAP: first partition pass fused into the degree
-                         //   scatter (3, graph2tree_dev), beside the degree pass (2), after it
-                         //   (1), in line (0)
+  int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
+                         //   after it (1), in line (0), fused into the degree scatter (3,
+                         //   graph2tree_dev; taken anyway from 2^31 records)
   int seq_compact = 1;   // SHEEP_SEQ_COMPACT: sort only the ids with degree > 0
   int sort_radix = 0;    // SHEEP_SORT (1 = "radix"): two radix passes instead of the hi bins
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)

@@ -92,8 +92,9 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
     (18, 29, 0, {"bin_scatter": 0, "bin_direct": 0}),  # stable bin scatter
-    (18, 30, 0, {"part_overlap": 2}),  # unfused: the first partition pass beside the degrees
-    (18, 31, 1, {"part_overlap": 0}),  # unfused, in line
+    (18, 30, 0, {"part_overlap": 3}),  # fused: the degree scatter partitions the records
+    (18, 32, 1, {"part_overlap": 3}),  # fused, FILE degrees
+    (18, 31, 1, {"part_overlap": 0}),  # the first partition pass in line
 ])
 def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
@@ -118,12 +119,14 @@ def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env)
 
 @pytest.mark.parametrize("n,m,mode", [((1 << 26) + 5, (1 << 22) + 12345, 0),
                                       ((1 << 25) + 77, (1 << 22) + 1, 1)])
-def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, n, m, mode):
+def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, options, n, m, mode):
     """The fused front half (launch_fh_front) with 64K-id buckets (n_ids > 2^25: the one-read
-    u16 histogram over the y ids then the x ids) and a ragged last chunk: seq, parent and pst
-    bit-exact in both degree conventions."""
+    u16 histogram over the records' y ids then the x ids) and a ragged last chunk: seq, parent
+    and pst bit-exact in both degree conventions."""
     import torch
     from sheep_amd import device
+
+    options(part_overlap=3)
 
     uv_d = device.powerlaw(n, m, 2.2, 80.0, 9 + mode)
     uv = uv_d.cpu().numpy().view(np.uint32).reshape(-1, 2)
