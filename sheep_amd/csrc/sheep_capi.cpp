@@ -308,7 +308,7 @@ static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
     require_records(m, "degree");
     uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", fh_tmp_words(m, n_ids) * 4);
     uint64_t* recs = (uint64_t*)c.scratch.get("e_items", m * 8);
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     uint32_t* st = stats ? stats : (uint32_t*)c.scratch.get("stats", 16);
     launch_fh_front(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, recs, pws, st, s);
     if (counted) HIP_CHECK(hipEventRecord(counted, s));
@@ -317,7 +317,7 @@ static bool degree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, uint32_t n_ids,
   // (ids beyond 2^26: launch_degree_bucketed takes the global-atomic pass, no offsets)
   if (degb_tmp_words(m, n_ids, nullptr, nullptr) > 1) require_endpoints(m, "degree");
   uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", degb_tmp_words(m, n_ids, nullptr, nullptr) * 4);
-  uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", 1024 * 4) : nullptr;
+  uint32_t* yhist = want_yhist ? (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4) : nullptr;
   return launch_degree_bucketed(d_uv, m, n_ids, mode, d_deg, d_selfc, c.d_err, tmp, s, yhist,
                                 counted, stats);
 }
@@ -724,7 +724,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     HIP_CHECK(hipEventRecord(c.bins_ev, s));
   }
   if (part) {
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
       HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
       launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
@@ -1016,11 +1016,11 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   const bool part = use_part(m);
   if (part) {
     if (part_done) {  // pass 1 ran beside the degree all-reduce and the sequence
-      uint32_t* pws = (uint32_t*)sc.get("part_ws", 1024 * 4);
+      uint32_t* pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
       HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
       launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
     } else {
-      uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", 1024 * 4);
+      uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
     }
     src = (const uint32_t*)items_b;
@@ -1232,7 +1232,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
                              overlap ? c.part_ev[0] : nullptr);
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", m * 8);
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
@@ -1535,7 +1535,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     require_records(m, "degree");  // its offsets count records, not endpoints
     uint32_t* tmp = (uint32_t*)c.scratch.get("degb_tmp", fh_tmp_words(m, n_ids) * 4);
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     fused = launch_fh_front(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, mid, pws,
                             stats, s, [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
   }
@@ -1548,7 +1548,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   if (fused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", 1024 * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     if (ov != 2) HIP_CHECK(hipEventRecord(c.part_ev[0], s));
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench

@@ -100,7 +100,7 @@ void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* 
                             uint32_t* start, uint32_t* end, uint32_t* pst, hipStream_t s);
 // Bucketed LDS degree histogram for large m (same result as launch_degree); selfc nullable.
 size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out);
-// yhist (nullable, 256 words): also counts the y digits of launch_part_gather's first pass
+// yhist (nullable, 1024 words): also counts the y digits of launch_part_gather's first pass
 // (n_rank = n_ids), so that pass needs no counting read; returns true when it did.
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
@@ -109,7 +109,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                             uint32_t* stats = nullptr /* [0] max degree, [1] zero-degree ids */);
 // Fused front half (graph2tree_dev): degrees (deg, selfc, stats as launch_degree_bucketed)
 // and the records (x, y) grouped by y bucket into recs (m u64), the x digits of
-// launch_part_second counted into part_ws[256, 512) — what launch_part_first produced.  tmp:
+// launch_part_second counted into part_ws[1024, 1280) — what launch_part_first produced.  tmp:
 // fh_tmp_words (1: not applicable, n_ids beyond 2^26).  False when not applicable.
 size_t fh_tmp_words(uint64_t m, uint32_t n_ids);
 bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,
@@ -172,7 +172,8 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
                         unsigned long long* bin_start, hipStream_t s,
                         unsigned long long* h_start = nullptr, hipEvent_t started = nullptr);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
-// m u64 scratch, ws: 1024 u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
+// m u64 scratch, ws: PART_WS_WORDS u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
+constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024;  // y / x digit counts, then u64 cursors
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
                         bool yhist_ready = false);

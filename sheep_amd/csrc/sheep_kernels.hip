@@ -341,17 +341,28 @@ static constexpr int DEGB_CHUNK = 32768;  // edges per chunk (<= 65536 endpoints
 static constexpr uint32_t DEGB_NB = 1024;
 static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgroup
 
-// Digit of the first partition pass of the rank gathers (launch_part_gather): 256 id ranges.
-__device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, 255u); }
+// Digits of the partition passes of the rank gathers (launch_part_gather): the first pass
+// (by y) cuts the ids into 1024 ranges (256 KB rank slices for the second pass's gathers), the
+// second (by x) into 256 (1 MB slices for the edge pass's).  part_ws layout (PART_WS_WORDS
+// u32): y-digit counts [0, 1024), x-digit counts [1024, 1280), u64 cursors from word 1280.
+static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_X = 1024, PW_CUR = 1280;
+template <uint32_t ND>
+__device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, ND - 1); }
+static int part_shift(uint32_t n_rank, uint32_t nd) {  // id >> shift < nd for ids < n_rank
+  int bits = 0, db = 0;
+  for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
+  for (uint32_t v = nd - 1; v; v >>= 1) ++db;
+  return bits > db ? bits - db : 0;
+}
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
              uint32_t NB, uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t* err,
              int psh, uint32_t* __restrict__ yhist, int tm) {
   __shared__ uint32_t hist[DEGB_NB];
-  __shared__ uint32_t yh[256];  // y digits of the later rank-gather partition (nullable yhist)
+  __shared__ uint32_t yh[PD_Y];  // y digits of the later rank-gather partition (nullable yhist)
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) hist[i] = 0;
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) yh[i] = 0;
+  for (uint32_t i = threadIdx.x; i < PD_Y; i += blockDim.x) yh[i] = 0;
   block_sync();
   const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
   const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
@@ -370,12 +381,12 @@ k_degb_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_
       if (e[u].x >= n_ids || e[u].y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
       atomicAdd(&hist[e[u].x >> SH], 1u);
       if (file_mode || e[u].x != e[u].y) atomicAdd(&hist[e[u].y >> SH], 1u);
-      if (yhist) atomicAdd(&yh[part_digit(e[u].y, psh)], 1u);
+      if (yhist) atomicAdd(&yh[part_digit<PD_Y>(e[u].y, psh)], 1u);
     }
   }
   block_sync();
   if (yhist)
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < PD_Y; i += blockDim.x)
       if (yh[i]) atomicAdd(&yhist[i], yh[i]);
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x)
     counts[tm ? (uint64_t)blockIdx.x * NB + i : (uint64_t)i * nchunks + blockIdx.x] = hist[i];
@@ -690,10 +701,8 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
     if (stats) launch_deg_stats(deg, n_ids, stats, s);
     return false;
   }
-  int pbits = 0;
-  for (uint32_t v = n_ids - 1; v; v >>= 1) ++pbits;
-  const int psh = pbits > 8 ? pbits - 8 : 0;  // as launch_part_gather with n_rank = n_ids
-  if (yhist) (void)hipMemsetAsync(yhist, 0, 256 * 4, s);
+  const int psh = part_shift(n_ids, PD_Y);  // as launch_part_gather with n_rank = n_ids
+  if (yhist) (void)hipMemsetAsync(yhist, 0, PD_Y * 4, s);
   if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
   uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   uint64_t cw = (uint64_t)NB * nchunks;
@@ -782,7 +791,7 @@ k_fh_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mo
       if (e[u].x >= n_ids || e[u].y >= n_ids) { atomicOr(err, ERR_RANGE); continue; }
       atomicAdd(&hy[e[u].y >> SH], 1u);
       if (file_mode || e[u].x != e[u].y) atomicAdd(&hx[e[u].x >> SH], 1u);
-      atomicAdd(&xd[part_digit(e[u].x, psh)], 1u);
+      atomicAdd(&xd[part_digit<PD_X>(e[u].x, psh)], 1u);
     }
   }
   block_sync();
@@ -926,12 +935,10 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
   uint16_t* epx = align16(bx + NB + 2);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
-  (void)hipMemsetAsync(part_ws, 0, 512 * 4, s);  // [256, 512): the x digits of k_part<1>
-  int pbits = 0;
-  for (uint32_t v = n_ids - 1; v; v >>= 1) ++pbits;
-  const int psh = pbits > 8 ? pbits - 8 : 0;  // as launch_part_gather with n_rank = n_ids
+  (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
+  const int psh = part_shift(n_ids, PD_X);  // as launch_part_second with n_rank = n_ids
   hipLaunchKernelGGL(k_fh_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
-                     n_ids, file_mode, SH, NB, cy, cx, err, psh, part_ws + 256);
+                     n_ids, file_mode, SH, NB, cy, cx, err, psh, part_ws + PW_X);
   tm_offsets(cy, oy, nchunks, NB, NB, gy, by, s);
   tm_offsets(cx, ox, nchunks, NB, NB, gx, bx, s);
   if (mark) mark(mark_arg, "degree_count");
@@ -1827,46 +1834,51 @@ static constexpr int PT0_ITEMS = PT_ITEMS, PT1_ITEMS = PT_ITEMS;
 // Global histogram of the y digits (the first partition's run sizes).
 __global__ void __launch_bounds__(PT_THREADS)
 k_part_count(const uint2* __restrict__ uv, uint64_t m, int sh, uint32_t* __restrict__ ghist) {
-  __shared__ uint32_t hist[256];
-  for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS) hist[i] = 0;
+  __shared__ uint32_t hist[PD_Y];
+  for (uint32_t i = threadIdx.x; i < PD_Y; i += PT_THREADS) hist[i] = 0;
   block_sync();
   for (uint64_t i = (uint64_t)blockIdx.x * PT_THREADS + threadIdx.x; i < m;
        i += (uint64_t)gridDim.x * PT_THREADS)
-    atomicAdd(&hist[part_digit(uv[i].y, sh)], 1u);
+    atomicAdd(&hist[part_digit<PD_Y>(uv[i].y, sh)], 1u);
   block_sync();
-  for (uint32_t i = threadIdx.x; i < 256; i += PT_THREADS)
+  for (uint32_t i = threadIdx.x; i < PD_Y; i += PT_THREADS)
     if (hist[i]) atomicAdd(&ghist[i], hist[i]);
 }
 
-// cursor[d] = exclusive prefix of hist (one block of 256 threads); hist is then cleared.
+// cursor[d] = exclusive prefix of hist (one block of ND threads); hist is then cleared.
+template <uint32_t ND>
 __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
-  __shared__ unsigned long long s[256];
+  __shared__ unsigned long long s[ND];
   uint32_t t = threadIdx.x;
   s[t] = hist[t];
   block_sync();
   if (t == 0) {
     unsigned long long run = 0;
-    for (int i = 0; i < 256; ++i) { unsigned long long v = s[i]; s[i] = run; run += v; }
+    for (uint32_t i = 0; i < ND; ++i) { unsigned long long v = s[i]; s[i] = run; run += v; }
   }
   block_sync();
   cursor[t] = s[t];
   hist[t] = 0;
 }
 
-template <int MODE, int NT, int IT>
+// ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1); NT >= ND (one digit per thread
+// in the scan).  MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
+template <int MODE, int NT, int IT, uint32_t ND>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
-       unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh,
+       unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
        const uint32_t* __restrict__ rank, uint32_t n_rank) {
+  static_assert(NT >= (int)ND, "one digit per thread in the scan");
   constexpr int PT_ITEMS = IT;
   constexpr int TILE = NT * PT_ITEMS;
   __shared__ uint64_t stage[TILE];
-  __shared__ uint32_t hist[256], tstart[256], hx[256], wsum[NT / 64];
-  __shared__ unsigned long long gbase[256];
+  __shared__ uint32_t hist[ND], tstart[ND], hx[MODE == 0 ? PD_X : 1], wsum[NT / 64];
+  __shared__ unsigned long long gbase[ND];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
   const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
-  if (t < 256) { hist[t] = 0; hx[t] = 0; }
+  if (t < (int)ND) hist[t] = 0;
+  if (MODE == 0 && t < (int)PD_X) hx[t] = 0;
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
 #pragma unroll
@@ -1893,21 +1905,21 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   for (int k = 0; k < PT_ITEMS; ++k) {
     if ((uint32_t)k * NT + t < tile_n) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
-      li[k] = atomicAdd(&hist[part_digit(key, sh)], 1u);
-      if (MODE == 0) atomicAdd(&hx[part_digit((uint32_t)rec[k], sh)], 1u);
+      li[k] = atomicAdd(&hist[part_digit<ND>(key, sh)], 1u);
+      if (MODE == 0) atomicAdd(&hx[part_digit<PD_X>((uint32_t)rec[k], shx)], 1u);
     }
   }
   block_sync();
-  if (t < 256) {
+  if (t < (int)ND) {
     uint32_t c = hist[t];
     uint32_t incl = wave_incl_scan(c);
     if (lane == 63) wsum[w] = incl;
     tstart[t] = incl - c;
     gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;
-    if (MODE == 0 && hx[t]) atomicAdd(&xhist[t], hx[t]);
   }
+  if (MODE == 0 && t < (int)PD_X && hx[t]) atomicAdd(&xhist[t], hx[t]);
   block_sync();
-  if (t < 256) {
+  if (t < (int)ND) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
     tstart[t] += add;
@@ -1917,53 +1929,48 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   for (int k = 0; k < PT_ITEMS; ++k) {
     if ((uint32_t)k * NT + t < tile_n) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
-      stage[tstart[part_digit(key, sh)] + li[k]] = rec[k];
+      stage[tstart[part_digit<ND>(key, sh)] + li[k]] = rec[k];
     }
   }
   block_sync();
   for (uint32_t j = t; j < tile_n; j += NT) {
     uint64_t r = stage[j];
-    uint32_t d = part_digit(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
+    uint32_t d = part_digit<ND>(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
     out[gbase[d] + (j - tstart[d])] = r;
   }
 }
 
-// uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: 512 u32 + 256 u64.
-static int part_shift(uint32_t n_rank) {
-  int bits = 0;
-  for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
-  return bits > 8 ? bits - 8 : 0;
-}
-
+// uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: PART_WS_WORDS.
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
                        uint32_t* ws, hipStream_t s, bool yhist_ready) {
   if (m == 0) return;
-  const int sh = part_shift(n_rank);
+  const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   uint32_t* yhist = ws;
-  uint32_t* xhist = ws + 256;
-  unsigned long long* cursor = (unsigned long long*)(ws + 512);
+  uint32_t* xhist = ws + PW_X;
+  unsigned long long* cursor = (unsigned long long*)(ws + PW_CUR);
   if (yhist_ready) {  // counted by the degree pass (launch_degree_bucketed)
-    (void)hipMemsetAsync(xhist, 0, 256 * 4, s);
+    (void)hipMemsetAsync(xhist, 0, PD_X * 4, s);
   } else {
-    (void)hipMemsetAsync(ws, 0, 512 * 4, s);
+    (void)hipMemsetAsync(ws, 0, PW_CUR * 4, s);
     hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
   }
-  hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, yhist, cursor);
+  hipLaunchKernelGGL(k_part_cursor<PD_Y>, dim3(1), dim3(PD_Y), 0, s, yhist, cursor);
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
-  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS>), dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m,
-                     mid, cursor, xhist, sh, (const uint32_t*)nullptr, n_rank);
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt), dim3(PT0_THREADS),
+                     0, s, (const uint64_t*)uv, m, mid, cursor, xhist, sh, shx,
+                     (const uint32_t*)nullptr, n_rank);
 }
 
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s) {
   if (m == 0) return;
-  const int sh = part_shift(n_rank);
-  uint32_t* xhist = ws + 256;
-  unsigned long long* cursor = (unsigned long long*)(ws + 512);
+  const int shx = part_shift(n_rank, PD_X);
+  uint32_t* xhist = ws + PW_X;
+  unsigned long long* cursor = (unsigned long long*)(ws + PW_CUR);
   uint64_t nt = (m + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
-  hipLaunchKernelGGL(k_part_cursor, dim3(1), dim3(256), 0, s, xhist, cursor);
-  hipLaunchKernelGGL((k_part<1, PT1_THREADS, PT1_ITEMS>), dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, m,
-                     pre, cursor, xhist, sh, rank, n_rank);
+  hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor);
+  hipLaunchKernelGGL((k_part<1, PT1_THREADS, PT1_ITEMS, PD_X>), dim3((unsigned)nt), dim3(PT1_THREADS),
+                     0, s, mid, m, pre, cursor, xhist, shx, shx, rank, n_rank);
 }
 
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
