@@ -343,8 +343,10 @@ static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgro
 
 // Digits of the partition passes of the rank gathers (launch_part_gather): the first pass
 // (by y) cuts the ids into 1024 ranges (256 KB rank slices for the second pass's gathers), the
-// second (by x) into 256 (1 MB slices for the edge pass's).  part_ws layout (PART_WS_WORDS
-// u32): y-digit counts [0, 1024), x-digit counts [1024, 1280), u64 cursors from word 1280.
+// second (by x) into 256 (1 MB slices for the edge pass's: 1024 x digits made the edge pass
+// 8.2 -> 7.7 ms but the second pass 5.6 -> 8.0 ms, its 8K-record tiles then writing 64-B
+// runs).  part_ws layout (PART_WS_WORDS u32): y-digit counts [0, 1024), x-digit counts
+// [1024, 1280), u64 cursors from word 1280.
 static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_X = 1024, PW_CUR = 1280;
 template <uint32_t ND>
 __device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, ND - 1); }
@@ -770,9 +772,9 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_fh_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
            uint32_t NB, uint32_t* __restrict__ cy, uint32_t* __restrict__ cx, uint32_t* err,
            int psh, uint32_t* __restrict__ xdig) {
-  __shared__ uint32_t hy[DEGB_NB], hx[DEGB_NB], xd[256];
+  __shared__ uint32_t hy[DEGB_NB], hx[DEGB_NB], xd[PD_X];
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) { hy[i] = 0; hx[i] = 0; }
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) xd[i] = 0;
+  for (uint32_t i = threadIdx.x; i < PD_X; i += blockDim.x) xd[i] = 0;
   block_sync();
   const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
   const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
@@ -795,7 +797,7 @@ k_fh_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mo
     }
   }
   block_sync();
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+  for (uint32_t i = threadIdx.x; i < PD_X; i += blockDim.x)
     if (xd[i]) atomicAdd(&xdig[i], xd[i]);
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) {
     cy[(uint64_t)blockIdx.x * NB + i] = hy[i];
@@ -1861,14 +1863,15 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
   hist[t] = 0;
 }
 
-// ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1); NT >= ND (one digit per thread
-// in the scan).  MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
+// ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1), ND / NT per thread in the scan.
+// MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
 template <int MODE, int NT, int IT, uint32_t ND>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
        const uint32_t* __restrict__ rank, uint32_t n_rank) {
-  static_assert(NT >= (int)ND, "one digit per thread in the scan");
+  static_assert(ND % NT == 0 || NT % ND == 0, "digits per thread");
+  constexpr int R = ND > (uint32_t)NT ? (int)ND / NT : 1;  // digits per thread in the scan
   constexpr int PT_ITEMS = IT;
   constexpr int TILE = NT * PT_ITEMS;
   __shared__ uint64_t stage[TILE];
@@ -1877,8 +1880,9 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
   const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
-  if (t < (int)ND) hist[t] = 0;
-  if (MODE == 0 && t < (int)PD_X) hx[t] = 0;
+  for (uint32_t i = t; i < ND; i += NT) hist[i] = 0;
+  if (MODE == 0)
+    for (uint32_t i = t; i < PD_X; i += NT) hx[i] = 0;
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
 #pragma unroll
@@ -1910,19 +1914,30 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
     }
   }
   block_sync();
-  if (t < (int)ND) {
-    uint32_t c = hist[t];
-    uint32_t incl = wave_incl_scan(c);
+  if (t * R < (int)ND) {  // digits [t R, t R + R): exclusive starts in the tile, global runs
+    uint32_t c[R], sum = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) { c[r] = hist[t * R + r]; sum += c[r]; }
+    const uint32_t incl = wave_incl_scan(sum);
     if (lane == 63) wsum[w] = incl;
-    tstart[t] = incl - c;
-    gbase[t] = c ? atomicAdd(&cursor[t], (unsigned long long)c) : 0ull;
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t d = t * R + r;
+      tstart[d] = run;
+      run += c[r];
+      gbase[d] = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
+    }
   }
-  if (MODE == 0 && t < (int)PD_X && hx[t]) atomicAdd(&xhist[t], hx[t]);
+  if (MODE == 0)
+    for (uint32_t i = t; i < PD_X; i += NT)
+      if (hx[i]) atomicAdd(&xhist[i], hx[i]);
   block_sync();
-  if (t < (int)ND) {
+  if (t * R < (int)ND) {
     uint32_t add = 0;
     for (int i = 0; i < w; ++i) add += wsum[i];
-    tstart[t] += add;
+#pragma unroll
+    for (int r = 0; r < R; ++r) tstart[t * R + r] += add;
   }
   block_sync();
 #pragma unroll
