@@ -912,6 +912,10 @@ struct Lockstep {
   uint32_t* gbits = nullptr;
   uint32_t* gx = nullptr;
   uint32_t* gsum = nullptr;  // the giant summary of the next map (launch_gb_sum, after the pick)
+  // The maps leave their union-find misses to the apply's refresh (as the one-GPU loop does)
+  // only for a one-rank group: with P ranks the refresh would repeat on every rank the finds
+  // that the maps split P ways.
+  bool defer = false;
   ~Lockstep() {
     for (auto& e : pick_ev)
       if (e) (void)hipEventDestroy(e);
@@ -1123,7 +1127,7 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
                 L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
                 L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
                 L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
-                false, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr,
+                L.defer, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr,
                 k >= 1 ? L.gsum : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
@@ -1254,6 +1258,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   Lockstep L;
   L.ctx = &c;
   L.scp = &c.scratch;
+  L.defer = comm.size() == 1 && knobs().kb_defer != 0;
   c.ls_live++;
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
@@ -1267,16 +1272,32 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   HIP_CHECK(hipStreamSynchronize(s));
   uint32_t nbk = 0, S = 0;
   ls_plan(L, counts.data(), &nbk, &S);
+  // The exchange buffers, sized once: a rank keeps at most one pair per record of the bucket,
+  // so the MAX over ranks and buckets of a rank's records in one bucket bounds every all-gather
+  // width (no allocation inside the loop).
+  uint64_t max_recs = 0;
+  for (uint32_t k = 0; k < nbk; ++k) {
+    const uint64_t a = L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second;
+    const uint64_t b = L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second;
+    max_recs = std::max<uint64_t>(max_recs, b - a);
+  }
+  int64_t* d_max = (int64_t*)c.scratch.get("mt_max", 8);
+  HIP_CHECK(hipMemcpyAsync(d_max, &max_recs, 8, hipMemcpyHostToDevice, s));
+  comm.allreduce_max_i64(d_max, 1, s);
+  HIP_CHECK(hipMemcpyAsync(&max_recs, d_max, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
   if (tm) tm->mark("binned");
   // The bucket loop, pipelined: bucket k+1 is mapped and exchanged on the side stream while
   // bucket k is applied on s.  The host waits once per bucket, for the MAX over the ranks of
   // the kept counts (the all-gather's size).
   const int P = comm.size();
   hipStream_t s2 = c.side;
-  uint64_t cap_send = (uint64_t)S + std::max<uint64_t>(m, 1);
+  const uint64_t cap_send = (uint64_t)S + std::max<uint64_t>(max_recs, 1);
   uint64_t* send = (uint64_t*)c.scratch.get("mt_send", cap_send * 8);
-  uint64_t* recv[2] = {nullptr, nullptr};
-  uint64_t recv_cap[2] = {0, 0};
+  uint64_t* recv[2] = {(uint64_t*)c.scratch.get("mt_recv0", (uint64_t)P * cap_send * 8),
+                       (uint64_t*)c.scratch.get("mt_recv1", (uint64_t)P * cap_send * 8)};
+  (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);  // ls_apply's unpacked pairs
+  L.kept_bytes = 0;
   int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;
@@ -1288,23 +1309,9 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     HIP_CHECK(hipStreamSynchronize(s2));
     const uint32_t cap = (uint32_t)*(const int64_t*)c.h_pinned;
     const uint64_t width = (uint64_t)S + cap;
-    if (width > cap_send) {  // another rank kept more pairs than this one has records
-      uint64_t* grown = nullptr;
-      HIP_CHECK(hipMalloc(&grown, width * 8));
-      HIP_CHECK(hipMemcpyAsync(grown, send, cap_send * 8, hipMemcpyDeviceToDevice, s2));
-      HIP_CHECK(hipStreamSynchronize(s2));
-      send = (uint64_t*)c.scratch.get("mt_send", width * 8);  // frees the old slot
-      HIP_CHECK(hipMemcpyAsync(send, grown, cap_send * 8, hipMemcpyDeviceToDevice, s2));
-      HIP_CHECK(hipStreamSynchronize(s2));
-      HIP_CHECK(hipFree(grown));
-      cap_send = width;
-    }
+    if (width > cap_send) throw ApiError(-EIO, "lockstep: kept pairs exceed the bucket's records");
     ls_pack(L, k, send, cap, s2);
     const int p = k & 1;
-    if (recv_cap[p] < (uint64_t)P * width) {  // bucket k-2 (its last reader) is applied
-      recv_cap[p] = std::max<uint64_t>((uint64_t)P * width, recv_cap[p] * 5 / 4);
-      recv[p] = (uint64_t*)c.scratch.get(p ? "mt_recv1" : "mt_recv0", recv_cap[p] * 8);
-    }
     comm.allgather_u64(send, recv[p], width, s2);
     HIP_CHECK(hipEventRecord(exchanged[p], s2));
     caps[p] = cap;
