@@ -189,7 +189,13 @@ int sheep_merge_forests_dev(const uint32_t* d_parents, uint32_t n_trees, uint32_
  *   sheep_ls_finish  d_parent (n_seq, identical on every rank) and d_pst (n_seq) of THIS
  *                    shard's records from its own degrees d_deg / d_selfc (sum over ranks =
  *                    the tree's pst_weight).  Synchronises.
- *   sheep_ls_free    releases the state. */
+ *   sheep_ls_free    releases the state.
+ * Split apply (optional, P >= 2; sheep_ls_split(handle, rank, P) once, before the first map):
+ * the spine and zipper of bucket k run only on rank k mod P; every rank still applies the
+ * union-find part, so the maps stay exact.  sheep_ls_finish then gives in d_parent only the
+ * forest edges of this rank's buckets (INVALID elsewhere); the ranks' forests are disjoint, so
+ * the caller's sum over ranks of (d_parent + 1) (u32, wrapping) is the tree's parent + 1. */
+int sheep_ls_split(void* handle, uint32_t rank, uint32_t n_ranks);
 int sheep_ls_begin(const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank, uint32_t n_rank,
                    const uint32_t* d_seq, uint32_t n_seq, const uint32_t* d_deg,
                    uint64_t* bin_counts_out, uint32_t* n_bins_out, void** handle_out,

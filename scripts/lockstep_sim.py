@@ -2,8 +2,9 @@
 """One-GPU simulation of the P-rank lockstep tree build: P shards of the same
 R-MAT graph held by one process (sheep_amd.dist.lockstep_local), checked bit-exact against the
 single-GPU graph2tree, with each rank's kernel time (map, apply) from HIP events.  The
-critical path without communication is max_r(map_r) + apply (every rank applies the same
-union).  One JSON line per P.
+critical path without communication is max_r(map_r) + max_r(apply_r) (every rank applies the
+union-find part of every bucket; with the split apply each bucket's zipper runs on its owner
+rank beside the loop, zip_ms_per_rank).  One JSON line per P.
 
     python scripts/lockstep_sim.py [--scale 26] [--P 2 4 8] [--reps 2]
 """
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--P", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--no-split", action="store_true",
+                    help="every rank runs every bucket's zipper (the replicated apply)")
     args = ap.parse_args()
     from sheep_amd import capi, device
     from sheep_amd.dist import lockstep_local, shard_bounds
@@ -43,7 +46,7 @@ def main():
             st = {}
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            s, p, w, n2 = lockstep_local(shards, n_ids, stats=st)
+            s, p, w, n2 = lockstep_local(shards, n_ids, stats=st, split=not args.no_split)
             torch.cuda.synchronize()
             wall = time.perf_counter() - t0
             ok = (n2 == n and torch.equal(s[:n], ref[0]) and torch.equal(p[:n], ref[1])
@@ -51,7 +54,10 @@ def main():
             rec = {"P": P, "scale": args.scale, "exact": ok, "wall_ms": 1e3 * wall,
                    "map_ms_per_rank": [round(x, 3) for x in st["kb_map"]],
                    "apply_ms": round(st["kb_apply"][0], 3), "buckets": int(st["kb_apply#"][0]),
-                   "critical_tree_ms": round(max(st["kb_map"]) + st["kb_apply"][0], 3),
+                   "critical_tree_ms": round(max(st["kb_map"]) + max(st["kb_apply"]), 3),
+                   "split": not args.no_split,
+                   "zip_ms_per_rank": [round(x, 3) for x in st.get("kb_zip", [])],
+                   "apply_ms_per_rank": [round(x, 3) for x in st["kb_apply"]],
                    "kept_pairs": st.get("kept", 0), "gathered_pairs": st.get("gathered", 0),
                    "K": os.environ.get("SHEEP_KB_BUCKETS", "auto"),
                    "single_gpu_tree_insert_ms": round(single.get("tree_insert", 0), 3)}

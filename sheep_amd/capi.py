@@ -78,6 +78,7 @@ def lib():
         "sheep_ls_begin": [u32p, c.c_uint64, u32p, c.c_uint32, u32p, c.c_uint32, u32p, vp, vp,
                            vp, vp],
         "sheep_ls_plan": [vp, vp, vp, vp],
+        "sheep_ls_split": [vp, c.c_uint32, c.c_uint32],
         "sheep_ls_map": [vp, c.c_uint32, vp, vp, vp, vp],
         "sheep_ls_pack": [vp, c.c_uint32, vp, c.c_uint32, vp],
         "sheep_ls_apply": [vp, c.c_uint32, vp, c.c_uint32, c.c_uint32, vp],

@@ -49,6 +49,7 @@ static const KnobDef kKnobs[] = {
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
+    {"ls_split", &Knobs::ls_split},
 };
 
 static Knobs g_knobs;
@@ -513,7 +514,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     launch_kb_map(sorted, seg ? seg->cstart[bk[k].second] : bk[k].second,
                   seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
                   anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
-                  lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, defer,
+                  lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, (int)defer,
                   st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr, k >= 1 ? gsum : nullptr);
     if (tm) tm->span_end(sp, st);
   };
@@ -916,7 +917,28 @@ struct Lockstep {
   // only for a one-rank group: with P ranks the refresh would repeat on every rank the finds
   // that the maps split P ways.
   bool defer = false;
+  // Split apply (P > 1 ranks, launch_ls_fold_union_label / launch_ls_zip): bucket k's spine and
+  // zipper run only on its owner rank (k mod P), on zs, from copies of the bucket's refreshed
+  // pairs and marks (two slots, by owned-bucket parity); every rank applies the union-find part.
+  // parent[] then holds this rank's buckets' forest edges only: the ranks' forests are disjoint
+  // and are summed by the caller.
+  bool split = false;
+  uint32_t rank = 0, P = 1, nzip = 0;
+  hipStream_t zs = nullptr;
+  uint64_t* zkept[2] = {nullptr, nullptr};
+  uint32_t *zbm[2] = {nullptr, nullptr}, *zn[2] = {nullptr, nullptr}, *zspq = nullptr;
+  hipEvent_t zready[2] = {nullptr, nullptr}, zdone[2] = {nullptr, nullptr};
+  bool zused[2] = {false, false};
+  size_t zkept_bytes[2] = {0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> zip_ev;
   ~Lockstep() {
+    if (zs) (void)hipStreamSynchronize(zs);
+    for (auto& e : zready)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : zdone)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : zip_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    if (zs) (void)hipStreamDestroy(zs);
     for (auto& e : pick_ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : map_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -1079,6 +1101,28 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   *nb_out = nb;
 }
 
+// The split apply for rank `rank` of P (P > 1; after ls_begin).  Its own buffers are taken from
+// the session's scratch; kept_hint: the largest P * cap the loop will apply (0: grown on demand).
+static void ls_set_split(Lockstep& L, uint32_t rank, uint32_t P, uint64_t kept_hint) {
+  if (P < 2 || rank >= P) throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
+  Scratch& sc = *L.scp;
+  L.split = true;
+  L.rank = rank;
+  L.P = P;
+  HIP_CHECK(hipStreamCreateWithFlags(&L.zs, hipStreamNonBlocking));
+  for (int z = 0; z < 2; ++z) {
+    L.zbm[z] = (uint32_t*)sc.get(z ? "ls_zbm1" : "ls_zbm0", L.bm_words * 4);
+    L.zn[z] = (uint32_t*)sc.get(z ? "ls_zn1" : "ls_zn0", 16);
+    if (kept_hint) {
+      L.zkept_bytes[z] = kept_hint * 8;
+      L.zkept[z] = (uint64_t*)sc.get(z ? "ls_zkept1" : "ls_zkept0", L.zkept_bytes[z]);
+    }
+    HIP_CHECK(hipEventCreateWithFlags(&L.zready[z], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&L.zdone[z], hipEventDisableTiming));
+  }
+  L.zspq = (uint32_t*)sc.get("ls_zspq", L.spq_words * 4);
+}
+
 static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_out,
                     uint32_t* ms_out) {
   const uint32_t nb = (uint32_t)L.bounds.size();
@@ -1127,7 +1171,8 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
                 L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
                 L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
                 L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
-                L.defer, s, L.direct ? &sg : nullptr, L.anc ? L.anc + (k & 1) : nullptr,
+                L.split ? 2 : (int)L.defer, s, L.direct ? &sg : nullptr,
+                L.anc ? L.anc + (k & 1) : nullptr,
                 k >= 1 ? L.gsum : nullptr);
   HIP_CHECK(hipEventRecord(ev.second, s));
   if (d_count) launch_ls_count(L.cnt_of(k) + 3, d_count, s);
@@ -1179,6 +1224,45 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     gslot = k + 1;
   }
   auto ev = L.span(L.apply_ev, s);
+  if (L.split) {
+    // Every rank: the marks (OR over ranks), the fold, the union of the pairs read straight
+    // from d_recv (their starts need no refresh for that), the labels.  The bucket's owner
+    // first unpacks the pairs into its slot and refreshes them there (the zipper needs the
+    // pre-bucket roots, against the union-find as bucket k-1 left it), then hands them to zs.
+    const bool ne = L.global_e[k] > 0;
+    const uint32_t* gx = L.gbits ? L.gx + (gslot & 1) : nullptr;
+    const uint32_t* anc_k = L.anc ? L.anc + (k & 1) : nullptr;
+    if (ne && k % L.P == L.rank) {
+      const int z = L.nzip++ & 1;
+      if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));  // the slot's last zipper
+      if (need > L.zkept_bytes[z]) {
+        HIP_CHECK(hipDeviceSynchronize());
+        L.zkept_bytes[z] = std::max(need, L.zkept_bytes[z] * 5 / 4);
+        L.zkept[z] = (uint64_t*)L.scp->get(z ? "ls_zkept1" : "ls_zkept0", L.zkept_bytes[z]);
+      }
+      launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, L.zkept[z], L.zn[z], s);
+      HIP_CHECK(hipMemcpyAsync(L.zbm[z] + w0, L.bm_of(k) + w0, (size_t)(w1 - w0 + 1) * 4,
+                               hipMemcpyDeviceToDevice, s));
+      launch_kb_refresh(L.zkept[z], L.zn[z], L.uf, L.label, L.zbm[z], B0, L.anchor(k), L.gbits, gx,
+                        anc_k, s);
+      launch_ls_gslot(L.uf, L.label, L.anchor(k), anc_k, L.zn[z] + 2, s);
+      HIP_CHECK(hipEventRecord(L.zready[z], s));
+      HIP_CHECK(hipStreamWaitEvent(L.zs, L.zready[z], 0));
+      auto zev = L.span(L.zip_ev, L.zs);
+      launch_ls_zip(L.zkept[z], L.zn[z], L.zbm[z], L.zspq, B0, B1, L.anchor(k) != INV, L.parent,
+                    L.jump, L.zs);
+      HIP_CHECK(hipEventRecord(zev.second, L.zs));
+      HIP_CHECK(hipEventRecord(L.zdone[z], L.zs));
+      L.zused[z] = true;
+    } else {
+      launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, nullptr, nullptr, s);
+    }
+    launch_ls_fold_union_label(ne, B0, B1, L.anchor(k), L.uf, L.label, d_recv, P, L.ms, cap,
+                               L.bm_of(k), L.cnt_of(k), L.gbits, gx, s, anc_k,
+                               L.anc ? L.anc + ((k + 1) & 1) : nullptr);
+    HIP_CHECK(hipEventRecord(ev.second, s));
+    return;
+  }
   launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
                   L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, L.gbits,
@@ -1190,6 +1274,8 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
 static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t* d_deg,
                       const uint32_t* d_selfc, int mode, uint32_t* d_parent, uint32_t* d_pst,
                       hipStream_t s) {
+  for (int z = 0; z < 2; ++z)  // split: this rank's zippers
+    if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));
   if (L.n_seq) {
     launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
     HIP_CHECK(hipMemcpyAsync(d_parent, L.parent, (size_t)L.n_seq * 4, hipMemcpyDeviceToDevice, s));
@@ -1205,10 +1291,13 @@ static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t
       t += ms;
     }
     c.timings.emplace_back(name, t);
-    c.timings.emplace_back(name == std::string("kb_map") ? "kb_map#" : "kb_apply#", (double)v.size());
+    const std::string nm(name);
+    c.timings.emplace_back(nm == "kb_map" ? "kb_map#" : nm == "kb_zip" ? "kb_zip#" : "kb_apply#",
+                           (double)v.size());
   };
   sum("kb_map", L.map_ev);
   sum("kb_apply", L.apply_ev);
+  if (L.split) sum("kb_zip", L.zip_ev);
 }
 
 // ---- graph2tree -i -r on one rank (the multi-GPU driver) ------------------------------------
@@ -1298,6 +1387,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
                        (uint64_t*)c.scratch.get("mt_recv1", (uint64_t)P * cap_send * 8)};
   (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);  // ls_apply's unpacked pairs
   L.kept_bytes = 0;
+  if (P > 1 && knobs().ls_split && n_seq) ls_set_split(L, (uint32_t)comm.rank(), (uint32_t)P, (uint64_t)P * cap_send);
   int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;
@@ -1332,6 +1422,11 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   }
   if (tm) tm->mark("tree");
   ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, d_pst, s);
+  if (L.split) {  // the owners' forests are disjoint: sum parent + 1 (INVALID + 1 = 0)
+    launch_add_u32(d_parent, n_seq, 1u, s);
+    comm.allreduce_sum_u32(d_parent, n_seq, s);
+    launch_add_u32(d_parent, n_seq, INV, s);
+  }
   comm.allreduce_sum_u32(d_pst, n_seq, s);
   HIP_CHECK(hipStreamSynchronize(s));
   if (tm) tm->mark("pst");
@@ -1908,6 +2003,15 @@ int sheep_ls_plan(void* handle, const uint64_t* global_bin_counts, uint32_t* n_b
   API_BEGIN
   if (!handle || !global_bin_counts) throw ApiError(-EINVAL, "null argument");
   ls_plan(*(Lockstep*)handle, global_bin_counts, n_buckets_out, mark_slots_out);
+  API_END
+}
+
+int sheep_ls_split(void* handle, uint32_t rank, uint32_t n_ranks) {
+  API_BEGIN
+  if (!handle) throw ApiError(-EINVAL, "null handle");
+  Lockstep& L = *(Lockstep*)handle;
+  if (L.split || !L.map_ev.empty()) throw ApiError(-EINVAL, "lockstep split: set once, before the first map");
+  if (L.n_seq) ls_set_split(L, rank, n_ranks, 0);
   API_END
 }
 

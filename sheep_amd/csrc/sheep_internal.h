@@ -61,6 +61,8 @@ struct Knobs {
   int kb_gsum = -1;      // SHEEP_KB_GSUM: the map tests 64-rank "all in the giant" blocks in LDS
                          //   first; -1 auto (from 2^27 records), 0, 1
   int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
+  int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
+                         //   rank (0: every rank applies every bucket's zipper)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
@@ -214,7 +216,8 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    unsigned long long* st, const uint32_t* bins /* nullable: hi bins */,
                    uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,
                    const uint32_t* gx /* its reference-vertex slot (nullable: no bitmap) */,
-                   bool defer /* misses kept as (b, a) for launch_kb_apply's refresh */,
+                   int defer /* 1: misses kept as (b, a) for launch_kb_apply's refresh;
+                                2: as (b, root of a) (split lockstep); 0: as (b, label) */,
                    hipStream_t s, const KbSegs* segs = nullptr,
                    const uint32_t* anc = nullptr /* device-picked anchor (launch_kb_pick) */,
                    const uint32_t* gsum = nullptr /* giant summary (launch_gb_sum) */);
@@ -243,12 +246,30 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      const uint32_t* anc_next = nullptr /* the next map's: its root is kept */);
 // Lockstep exchange of one bucket (sheep_ls_*): pack this rank's mark words [w0, w1] (ms u64
 // slots) and kept pairs (padded to cap) for an all-gather; unpack P such blocks into the
-// bitmap (OR) and a contiguous kept array, setting *n_kept = P * cap.
+// bitmap (OR) and a contiguous kept array, setting *n_kept = P * cap (kept and n_kept
+// nullable: the marks only).
 void launch_ls_pack(const uint32_t* bitmap, uint32_t w0, uint32_t w1, uint32_t ms, uint64_t* send,
                     const uint32_t* n_kept /* device */, uint32_t cap, hipStream_t s);
 void launch_ls_count(const uint32_t* n_kept, long long* out, hipStream_t s);
 void launch_ls_unpack(const uint64_t* recv, uint32_t P, uint32_t ms, uint32_t cap, uint32_t* bitmap,
                       uint32_t w0, uint32_t w1, uint64_t* kept, uint32_t* n_kept, hipStream_t s);
+// Split lockstep apply (P > 1; see sheep_kernels.hip): the refresh alone; G of the bucket's
+// giant into *gslot; every rank's union-find part (fold, union of the kept pairs, labels;
+// counters reset); the owner's spine + zipper over its copies (zn: n_kept, n_spine, G).
+void launch_kb_refresh(uint64_t* kept, const uint32_t* n_kept, uint32_t* uf, const uint32_t* label,
+                       uint32_t* bitmap, uint32_t B0, uint32_t anchor, uint32_t* gbits,
+                       const uint32_t* gx, const uint32_t* anc, hipStream_t s);
+void launch_ls_gslot(const uint32_t* uf, const uint32_t* label, uint32_t anchor, const uint32_t* anc,
+                     uint32_t* gslot, hipStream_t s);
+void launch_ls_fold_union_label(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor,
+                                uint32_t* uf, uint32_t* label, const uint64_t* recv, uint32_t P,
+                                uint32_t ms, uint32_t cap, uint32_t* bitmap, uint32_t* counters,
+                                uint32_t* gbits, const uint32_t* gx, hipStream_t s,
+                                const uint32_t* anc, const uint32_t* anc_next);
+void launch_ls_zip(const uint64_t* zkept, uint32_t* zn, const uint32_t* zbm, uint32_t* zspq,
+                   uint32_t B0, uint32_t B1, bool has_anchor, uint32_t* parent, uint32_t* jump,
+                   hipStream_t s);
+void launch_add_u32(uint32_t* p, uint64_t n, uint32_t d, hipStream_t s);  // p[i] += d (wraps)
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
 // Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)

@@ -2544,7 +2544,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     if (STATS) misses += (uint64_t)__popc(miss);
     // 2. the misses' finds (path halving), all chains of the lane advanced together — unless
     // they are deferred: then a miss is kept as (b, a) and k_kb_refresh resolves it
-    for (uint32_t act = defer ? 0u : miss; act;) {
+    for (uint32_t act = defer == 1 ? 0u : miss; act;) {
       uint32_t p[R], gp[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) p[r] = ((act >> r) & 1) ? uf[x[r]] : 0u;
@@ -2569,14 +2569,17 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     uint32_t lab[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if (!defer && ((miss >> r) & 1) && x[r] == RG) {
+      if (defer != 1 && ((miss >> r) & 1) && x[r] == RG) {
         giant |= 1u << r;
         if (use_bm) {
           const uint32_t a = (uint32_t)it[r];
           atomicOr(&gbits[a >> 5], 1u << (a & 31));
         }
       }
-      lab[r] = (!defer && ((miss & ~giant) >> r) & 1) ? label[x[r]] : (uint32_t)it[r];
+      // defer 2 (split lockstep): the root itself — the ranks' unions need no more, and the
+      // bucket's owner refreshes its pairs to the pre-bucket etree roots anyway
+      lab[r] = (defer == 0 && ((miss & ~giant) >> r) & 1) ? label[x[r]]
+               : (defer == 2 && ((miss & ~giant) >> r) & 1) ? x[r] : (uint32_t)it[r];
     }
     uint32_t nout = 0;
 #pragma unroll
@@ -2772,14 +2775,17 @@ k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_p
 // ranks (already in one tree).  gbits (nullable): the marked ranks are giant members; when
 // the bitmap's reference vertex *gx lies in the anchor's component they are set there too
 // (see k_kb_map).
+// Split lockstep (P ranks, launch_ls_apply_split): CHAIN writes only the forest part (parent,
+// spq: the bucket's zipper owner), FOLD only the union-find part (uf, gbits: every rank).
+template <bool CHAIN, bool FOLD>
 __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
                            uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit,
                            uint32_t* uf, uint32_t anchor, uint32_t* gbits,
                            const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc) {
   const uint32_t w0 = B0 >> 5, w1 = (B1 - 1) >> 5;
-  const uint32_t R = uf_find_ro(uf, anchor_rank(anchor, anc));
-  const uint32_t X = gbits ? *gx : INV;
-  const bool set_g = X != INV && uf_find_ro(uf, X) == R;
+  const uint32_t R = FOLD ? uf_find_ro(uf, anchor_rank(anchor, anc)) : INV;
+  const uint32_t X = (FOLD && gbits) ? *gx : INV;
+  const bool set_g = FOLD && X != INV && uf_find_ro(uf, X) == R;
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
        w += gridDim.x * blockDim.x) {
     uint32_t bits = word_in(bitmap, w, B0, B1);
@@ -2787,15 +2793,16 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
     if (set_g) atomicOr(&gbits[w], bits);
     uint32_t cur = (w << 5) + __ffs(bits) - 1;
     const uint32_t first = cur;
-    uf[cur] = R;
+    if (FOLD) uf[cur] = R;
     bits &= bits - 1;
     while (bits) {
       uint32_t nx = (w << 5) + __ffs(bits) - 1;
       bits &= bits - 1;
-      parent[cur] = nx;
-      uf[nx] = R;
+      if (CHAIN) parent[cur] = nx;
+      if (FOLD) uf[nx] = R;
       cur = nx;
     }
+    if (!CHAIN) continue;
     for (uint32_t v = w + 1, k = 0; v <= w1 && k < limit; ++v, ++k) {
       uint32_t nb = word_in(bitmap, v, B0, B1);
       if (nb) { parent[cur] = (v << 5) + __ffs(nb) - 1; break; }
@@ -2860,15 +2867,19 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
 
 // The kb in-bucket pass: the spine queue, then the kept (b, g) pairs of the bucket, through
 // the balanced lane queue with the spine rules (SpineInfo), recording pre-bucket roots it links.
-template <bool STATS>
+// REC = false (split lockstep, the bucket's zipper owner): no linked roots are recorded (every
+// rank unions the pairs themselves), and G comes from *gslot, captured before the bucket's
+// union-find changed (anchor != INV means there is one).
+template <bool STATS, bool REC = true>
 __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __restrict__ n_kept,
                          const uint32_t* __restrict__ bitmap, const uint32_t* __restrict__ spq,
                          const uint32_t* __restrict__ n_spine, uint32_t B0, uint32_t B1,
                          uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* parent,
                          uint32_t* jump, unsigned long long* stats, uint32_t* linked,
                          uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
-                         uint32_t qchunk, const uint32_t* __restrict__ anc) {
-  constexpr uint32_t LCAP = 2048;  // (512: RMAT-26 tree 16.7 -> 18.2 ms)
+                         uint32_t qchunk, const uint32_t* __restrict__ anc,
+                         const uint32_t* __restrict__ gslot = nullptr) {
+  constexpr uint32_t LCAP = REC ? 2048 : 1;  // (512: RMAT-26 tree 16.7 -> 18.2 ms)
   __shared__ uint32_t lbuf[LCAP];
   __shared__ uint32_t lcnt, lbase;
   if (threadIdx.x == 0) lcnt = 0;
@@ -2882,21 +2893,22 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   rec.lcap = LCAP;
   EdgeSrc src{kept};
   const uint64_t nk = *n_kept;
-  anchor = anchor_rank(anchor, anc);
+  if (REC) anchor = anchor_rank(anchor, anc);
   if (anchor != INV) {
     SpineInfo sp;
     sp.bitmap = bitmap;
     sp.B0 = B0;
     sp.B1 = B1;
-    sp.G = label[uf_find_ro(uf, anchor)];
+    sp.G = REC ? label[uf_find_ro(uf, anchor)] : *gslot;
     sp.limit = scan_limit;
     src.spq = spq;
     src.G = sp.G;
     src.np = *n_spine;
-    tree_queue_body<0, 1, STATS, true, true>(src, src.np + nk, parent, jump, stats, rec, qchunk, sp);
+    tree_queue_body<0, 1, STATS, REC, true>(src, src.np + nk, parent, jump, stats, rec, qchunk, sp);
   } else {
-    tree_queue_body<0, 1, STATS, true, false>(src, nk, parent, jump, stats, rec, qchunk);
+    tree_queue_body<0, 1, STATS, REC, false>(src, nk, parent, jump, stats, rec, qchunk);
   }
+  if (!REC) return;
   // the block's staged linked roots: one reservation, a coalesced copy
   block_sync();
   const uint32_t n = min(lcnt, LCAP);
@@ -3031,7 +3043,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
                    uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
-                   const uint32_t* gx, bool defer, hipStream_t s, const KbSegs* segs,
+                   const uint32_t* gx, int defer, hipStream_t s, const KbSegs* segs,
                    const uint32_t* anc, const uint32_t* gsum) {
   // segs: e_begin / e_end bound the bucket's records (the capacity of its bins)
   if (e_end <= e_begin) return;
@@ -3053,7 +3065,7 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   const uint32_t gs_w0 = w_end - gs_words;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), gs_words * 4, s, items, e_begin, e_end, sg,
                      B0, gshift, uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx, (int)defer, anc, gsum, gs_words, gs_w0);
+                     gx ? gbits : nullptr, gx, defer, anc, gsum, gs_words, gs_w0);
 }
 
 void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,
@@ -3089,7 +3101,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                          uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc,
                          knobs().kb_drop);
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
-      hipLaunchKernelGGL(k_kb_spine, dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
+      hipLaunchKernelGGL((k_kb_spine<true, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
                          uf, anchor, gbits, gx, anc);
     auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
@@ -3100,7 +3112,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
-                       anchor, scan_limit, qchunk, anc);
+                       anchor, scan_limit, qchunk, anc, (const uint32_t*)nullptr);
   }
   // giant fold: the marks are relative to the anchor's component; its root R_a may later be
   // linked below the union's R (pipelined: different anchors) — the folded ranks follow it
@@ -3115,6 +3127,150 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for((uint64_t)(B1 - B0) + 64)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold,
                      gbits, gx);
+}
+
+void launch_kb_refresh(uint64_t* kept, const uint32_t* n_kept, uint32_t* uf, const uint32_t* label,
+                       uint32_t* bitmap, uint32_t B0, uint32_t anchor, uint32_t* gbits,
+                       const uint32_t* gx, const uint32_t* anc, hipStream_t s) {
+  if (!gx) gbits = nullptr;
+  hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, n_kept, uf, label, bitmap,
+                     B0, anchor, gbits, gx, anc, knobs().kb_drop);
+}
+
+// ---- split lockstep apply (P ranks; sheep_capi.cpp ls_apply) ------------------------------
+// The zipper of bucket [B0, B1) reads and writes parent[] / jump[] only at the pre-bucket roots
+// its pairs start from (parent INVALID until this bucket) and at the bucket's own ranks (parent
+// INVALID until this bucket); no other bucket's zipper touches those entries.  So with P ranks
+// one owner rank runs a bucket's spine and zipper (on its own stream, off the loop's critical
+// path), and every rank keeps only the union-find current: the fold of the marks, the union of
+// the kept pairs themselves (not of the forest edges the zipper made) and the labels.  The
+// owners' forests are disjoint and summed at the end (parent + 1, INVALID + 1 = 0).
+
+// G for the owner's zipper: the giant's elimination-tree root at B0, before this bucket's union.
+__global__ void k_ls_gslot(const uint32_t* uf, const uint32_t* __restrict__ label, uint32_t anchor,
+                           const uint32_t* __restrict__ anc, uint32_t* gslot) {
+  anchor = anchor_rank(anchor, anc);
+  *gslot = anchor != INV ? label[uf_find_ro(uf, anchor)] : INV;
+}
+
+// union(g, b) for every kept pair of the P all-gathered contributions (recv, as k_ls_unpack
+// reads it), straight from the exchange buffer.  g is the map's start — a vertex of the pair's
+// component at B0, possibly stale, which the union does not mind (only the owner's zipper needs
+// the refreshed pre-bucket root).  R (the next map's giant root) is never linked below another.
+__global__ void k_ls_union_pairs(const uint64_t* __restrict__ recv, uint32_t P, uint32_t ms,
+                                 uint32_t cap, uint32_t* uf, uint32_t anchor,
+                                 const uint32_t* __restrict__ anc) {
+  anchor = anchor_rank(anchor, anc);
+  const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  const uint64_t stride = (uint64_t)ms + cap, total = (uint64_t)P * cap;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = j / cap, q = j - r * cap;
+    const uint64_t it = recv[r * stride + ms + q];
+    const uint32_t b = (uint32_t)(it >> 32);
+    if (b != INV) uf_union(uf, (uint32_t)it, b, R);
+  }
+}
+
+// Labels without the forest: every component this bucket touched holds one of its ranks, so its
+// label (its maximum rank = its elimination-tree root) is the max over the bucket's ranks in it.
+// One atomicMax per run of equal roots in consecutive lanes, and one per block for R (the giant:
+// most ranks).  gbits / clearing / counters as k_kb_label.
+__global__ void __launch_bounds__(BLOCK)
+k_ls_label(uint32_t* uf, uint32_t* label, uint32_t B0, uint32_t B1, uint32_t* counters,
+           uint32_t* bitmap, uint32_t* gbits, const uint32_t* __restrict__ gx, uint32_t anchor,
+           const uint32_t* __restrict__ anc) {
+  __shared__ uint32_t s_max;
+  anchor = anchor_rank(anchor, anc);
+  const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  const uint32_t X = gbits ? *gx : INV;
+  const uint32_t RX = X != INV ? uf_find_ro(uf, X) : INV;
+  if (threadIdx.x == 0) s_max = 0;
+  block_sync();
+  uint32_t rmax = 0;
+  const int lane = threadIdx.x & 63;
+  const uint32_t v0 = B0 & ~63u;  // waves cover whole 64-rank (two-word) groups
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; v0 + (uint64_t)i < B1 + 63;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t v = v0 + i;
+    const bool in_b = v >= B0 && v < B1;
+    const uint32_t rt = in_b ? uf_find<false>(uf, v) : INV;
+    const uint32_t nxt = (uint32_t)__shfl_down((int)rt, 1);
+    if (in_b) {
+      if (rt == R) rmax = max(rmax, v);
+      else if (lane == 63 || nxt != rt) atomicMax(&label[rt], v);
+    }
+    if (X != INV) {
+      const uint64_t bal = __ballot(in_b && rt == RX);
+      if (lane == 0 && (uint32_t)bal) atomicOr(&gbits[v >> 5], (uint32_t)bal);
+      if (lane == 32 && (uint32_t)(bal >> 32)) atomicOr(&gbits[v >> 5], (uint32_t)(bal >> 32));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
+  if (lane == 0 && rmax) atomicMax(&s_max, rmax);
+  block_sync();
+  if (threadIdx.x == 0 && s_max) atomicMax(&label[R], s_max);
+  for (uint32_t w = (B0 >> 5) + blockIdx.x * blockDim.x + threadIdx.x; w < ((B1 + 31) >> 5);
+       w += gridDim.x * blockDim.x)
+    bitmap[w] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { counters[1] = 0; counters[2] = 0; counters[3] = 0; }
+}
+
+void launch_ls_gslot(const uint32_t* uf, const uint32_t* label, uint32_t anchor, const uint32_t* anc,
+                     uint32_t* gslot, hipStream_t s) {
+  hipLaunchKernelGGL(k_ls_gslot, dim3(1), dim3(1), 0, s, uf, label, anchor, anc, gslot);
+}
+
+void launch_ls_fold_union_label(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor,
+                                uint32_t* uf, uint32_t* label, const uint64_t* recv, uint32_t P,
+                                uint32_t ms, uint32_t cap, uint32_t* bitmap, uint32_t* counters,
+                                uint32_t* gbits, const uint32_t* gx, hipStream_t s,
+                                const uint32_t* anc, const uint32_t* anc_next) {
+  if (!gx) gbits = nullptr;
+  const uint32_t anchor_next = B0 > 0 ? B0 - 1 : INV;
+  if (nonempty) {
+    if (anchor != INV && B1 > B0)  // the marked ranks go under the anchor's root (no forest)
+      hipLaunchKernelGGL((k_kb_spine<false, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)),
+                         dim3(BLOCK), 0, s, (const uint32_t*)bitmap, B0, B1, nullptr, nullptr,
+                         nullptr, 0u, uf, anchor, gbits, gx, anc);
+    if (cap)
+      hipLaunchKernelGGL(k_ls_union_pairs, dim3(MAX_GRID), dim3(BLOCK), 0, s, recv, P, ms, cap, uf,
+                         anchor_next, anc_next);
+  }
+  if (B1 > B0)
+    hipLaunchKernelGGL(k_ls_label, dim3(grid_for((uint64_t)(B1 - B0) + 128)), dim3(BLOCK), 0, s, uf,
+                       label, B0, B1, counters, bitmap, gbits, gx, anchor_next, anc_next);
+  else
+    hipLaunchKernelGGL(k_kb_label, dim3(1), dim3(BLOCK), 0, s, (const uint32_t*)nullptr, uf, label, B0,
+                       B1, counters, bitmap, 1, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+}
+
+// The owner's half: spine (forest part) and zipper of one bucket over its copies of the kept
+// pairs (zn[0] of them) and of the bucket's mark words; zn[1] = spine queue length (zeroed
+// here), zn[2] = G (launch_ls_gslot; INV: no giant).
+void launch_ls_zip(const uint64_t* zkept, uint32_t* zn, const uint32_t* zbm, uint32_t* zspq,
+                   uint32_t B0, uint32_t B1, bool has_anchor, uint32_t* parent, uint32_t* jump,
+                   hipStream_t s) {
+  (void)hipMemsetAsync(zn + 1, 0, 4, s);
+  if (has_anchor && B1 > B0)
+    hipLaunchKernelGGL((k_kb_spine<true, false>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)),
+                       dim3(BLOCK), 0, s, zbm, B0, B1, parent, zspq, zn + 1, 64u, nullptr, 0u,
+                       nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+  hipLaunchKernelGGL((k_kb_zip<false, false>), dim3(MAX_GRID), dim3(BLOCK), 0, s, zkept,
+                     (const uint32_t*)zn, zbm, (const uint32_t*)zspq, (const uint32_t*)(zn + 1), B0, B1,
+                     nullptr, (const uint32_t*)nullptr, parent, jump, nullptr, nullptr, nullptr,
+                     has_anchor ? 0u : INV, 64u, 256u, (const uint32_t*)nullptr,
+                     (const uint32_t*)(zn + 2));
+}
+
+__global__ void k_add_u32(uint32_t* p, uint64_t n, uint32_t d) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] += d;
+}
+
+void launch_add_u32(uint32_t* p, uint64_t n, uint32_t d, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_add_u32, dim3(grid_for(n)), dim3(BLOCK), 0, s, p, n, d);
 }
 
 // ---- lockstep exchange (multi-GPU kb loop, sheep_ls_*) -----------------------------------
@@ -3154,7 +3310,7 @@ __global__ void k_ls_unpack(const uint64_t* __restrict__ recv, uint32_t P, uint3
                             uint64_t* __restrict__ kept, uint32_t* n_kept) {
   const uint64_t stride = (uint64_t)ms + cap;
   const uint32_t nw = w1 - w0 + 1;
-  const uint64_t total = (uint64_t)nw + (uint64_t)P * cap;
+  const uint64_t total = (uint64_t)nw + (kept ? (uint64_t)P * cap : 0ull);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
     if (i < nw) {
@@ -3169,7 +3325,7 @@ __global__ void k_ls_unpack(const uint64_t* __restrict__ recv, uint32_t P, uint3
       kept[j] = recv[r * stride + ms + q];
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_kept = P * cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n_kept) *n_kept = P * cap;
 }
 
 void launch_ls_pack(const uint32_t* bitmap, uint32_t w0, uint32_t w1, uint32_t ms, uint64_t* send,
@@ -3182,7 +3338,7 @@ void launch_ls_pack(const uint32_t* bitmap, uint32_t w0, uint32_t w1, uint32_t m
 
 void launch_ls_unpack(const uint64_t* recv, uint32_t P, uint32_t ms, uint32_t cap, uint32_t* bitmap,
                       uint32_t w0, uint32_t w1, uint64_t* kept, uint32_t* n_kept, hipStream_t s) {
-  const uint64_t total = (uint64_t)(w1 - w0 + 1) + (uint64_t)P * cap;
+  const uint64_t total = (uint64_t)(w1 - w0 + 1) + (kept ? (uint64_t)P * cap : 0ull);
   hipLaunchKernelGGL(k_ls_unpack, dim3(grid_for(total)), dim3(BLOCK), 0, s, recv, P, ms, cap, bitmap,
                      w0, w1, kept, n_kept);
 }

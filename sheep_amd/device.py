@@ -138,6 +138,11 @@ class Lockstep:
         self.slots = ms.value
         return nbk.value, ms.value
 
+    def split(self, rank, n_ranks):
+        """Split apply (n_ranks >= 2): this rank runs the zipper of buckets k = rank mod P only;
+        finish() then returns its buckets' forest edges (the ranks' forests are disjoint)."""
+        capi.call("sheep_ls_split", self.h, rank, n_ranks)
+
     def map(self, k, send, count=None):
         """Map bucket k into send; with ``count`` (cuda int64 tensor) the kept-pair count is
         written there (no synchronisation) and None returned, else it is returned."""

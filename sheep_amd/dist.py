@@ -139,7 +139,7 @@ def _lockstep_loop_pipelined(ls, nbk, slots, m_local, world, dev, group):
     main.wait_stream(side)
 
 
-def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
+def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None, split=True):
     """graph2tree -i -r without partial trees (the default for P > 1).
 
     Steps 1-2 as build_tree_sharded.  Then every rank bins ITS records by hi (bins from the
@@ -148,6 +148,9 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     ranks are all-gathered over RCCL, and every rank applies all of them, so the replicas stay
     identical and every rank ends with the whole elimination tree.  pst_weight is the sum of
     the ranks' own pst (one sum-reduce to rank 0, as mpi_merge's merge adds them).
+    split (P > 1, when the session supports it): every rank applies the union-find part of
+    every bucket but the zipper of its own buckets only (k mod P); the disjoint forests are
+    summed at the end.
     Returns (seq, parent, pst, n_seq) on rank 0 and (seq, parent, None, n_seq) elsewhere."""
     import numpy as np
 
@@ -165,6 +168,9 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
         if world > 1:
             dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
         nbk, slots = ls.plan(counts.cpu().numpy())
+        split = world > 1 and split and hasattr(ls, "split")
+        if split:  # bucket k's zipper on rank k mod P only (sheep_ls_split)
+            ls.split(rank, world)
         if timings is not None:
             timings["binned"] = ops.now()
         if dist.is_initialized() and dev.type == "cuda":
@@ -174,6 +180,11 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
         parent, pst = ls.finish(seq, deg_local, selfc, mode)
     finally:
         ls.free()
+    if split:  # the ranks' forests are disjoint: sum parent + 1 (INVALID + 1 = 0)
+        p = _i32(parent[:n_seq])
+        p.add_(1)
+        dist.all_reduce(p, op=dist.ReduceOp.SUM, group=group)
+        p.sub_(1)
     if timings is not None:
         timings["tree"] = ops.now()
     if world > 1:
@@ -181,7 +192,7 @@ def build_tree_lockstep(uv_shard, n_ids, ops, mode=0, group=None, timings=None):
     return seq, parent, (pst if rank == 0 else None), n_seq
 
 
-def lockstep_local(shards, n_ids, mode=0, stats=None):
+def lockstep_local(shards, n_ids, mode=0, stats=None, split=True):
     """The lockstep build of build_tree_lockstep for P shards held by ONE process on one
     device (the all-gathers become device copies): the one-GPU rehearsal of the P-rank path.
     stats (dict, optional) receives per-rank kernel times {"kb_map": [...], "kb_apply": [...]}.
@@ -202,6 +213,10 @@ def lockstep_local(shards, n_ids, mode=0, stats=None):
         g = np.sum([s.bin_counts for s in sess], axis=0)
         plans = [s.plan(g) for s in sess]
         nbk, slots = plans[0]
+        split = split and P > 1
+        if split:
+            for r, s in enumerate(sess):
+                s.split(r, P)
         sends = [torch.empty(slots + max(uv.shape[0], 1), dtype=torch.int64, device=dev)
                  for uv in shards]
         for k in range(nbk):
@@ -226,12 +241,18 @@ def lockstep_local(shards, n_ids, mode=0, stats=None):
             if stats is not None:
                 for name, ms in capi.last_timings():
                     stats.setdefault(name, []).append(ms)
+            if split:  # disjoint forests: sum parent + 1 (INVALID + 1 = 0)
+                p.view(torch.int32).add_(1)
             if parent is None:
                 parent, pst = p, w
             else:
-                if not torch.equal(parent[:n_seq], p[:n_seq]):
+                if split:
+                    parent.view(torch.int32).add_(p.view(torch.int32))
+                elif not torch.equal(parent[:n_seq], p[:n_seq]):
                     raise RuntimeError("lockstep replicas diverged at rank %d" % r)
                 pst.view(torch.int32).add_(w.view(torch.int32))
+        if split:
+            parent.view(torch.int32).sub_(1)
     finally:
         for s in sess:
             s.free()
