@@ -39,13 +39,12 @@ struct KnobDef {
 static const KnobDef kKnobs[] = {
     {"degree", &Knobs::degree},           {"edge_part", &Knobs::edge_part},
     {"part_overlap", &Knobs::part_overlap}, {"seq_compact", &Knobs::seq_compact},
-    {"sort", &Knobs::sort_radix},         {"kb_buckets", &Knobs::kb_buckets},
+    {"kb_buckets", &Knobs::kb_buckets},
     {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
     {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},
     {"kb_defer", &Knobs::kb_defer},
     {"degb_plain", &Knobs::degb_plain},   {"degb_hist", &Knobs::degb_hist16},
-    {"bin_tm", &Knobs::bin_tm},           {"bin_scatter", &Knobs::bin_scatter},
-    {"ep_plain", &Knobs::ep_plain},       {"tree_stats", &Knobs::tree_stats},
+    {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
@@ -63,8 +62,6 @@ static void load_knobs_from_env() {
     if (!v) continue;
     if (d.field == &Knobs::degree)  // "atomic" / "bucketed" (or the number)
       g_knobs.degree = !strcmp(v, "atomic") ? 1 : !strcmp(v, "bucketed") ? 2 : atoi(v);
-    else if (d.field == &Knobs::sort_radix)
-      g_knobs.sort_radix = !strcmp(v, "radix") ? 1 : atoi(v);
     else
       g_knobs.*d.field = atoi(v);
   }
@@ -706,7 +703,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   bool part = use_part(m);
   const uint32_t* src = d_uv;
   // Hi bins (one scatter pass) when the degrees are at hand; else the two-pass radix sort.
-  const bool use_bins = pst_count && m >= (1ull << 20) && n_seq > 256 && !knobs().sort_radix;
+  const bool use_bins = pst_count && m >= (1ull << 20) && n_seq > 256;
   // The bins come from the chunk degree sums (seq order): they are summed and copied to the
   // host BEFORE the second partition pass is enqueued, so the host cuts the bins while the GPU
   // runs that pass instead of idling for the round trip.
@@ -1104,7 +1101,8 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
 // The split apply for rank `rank` of P (P > 1; after ls_begin).  Its own buffers are taken from
 // the session's scratch; kept_hint: the largest P * cap the loop will apply (0: grown on demand).
 static void ls_set_split(Lockstep& L, uint32_t rank, uint32_t P, uint64_t kept_hint) {
-  if (P < 2 || rank >= P) throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
+  if ((P < 2 && knobs().ls_split != 2) || rank >= P)
+    throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
   Scratch& sc = *L.scp;
   L.split = true;
   L.rank = rank;
@@ -1387,7 +1385,8 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
                        (uint64_t*)c.scratch.get("mt_recv1", (uint64_t)P * cap_send * 8)};
   (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);  // ls_apply's unpacked pairs
   L.kept_bytes = 0;
-  if (P > 1 && knobs().ls_split && n_seq) ls_set_split(L, (uint32_t)comm.rank(), (uint32_t)P, (uint64_t)P * cap_send);
+  if (((P > 1 && knobs().ls_split) || knobs().ls_split == 2) && n_seq)  // 2: also one rank (lab)
+    ls_set_split(L, (uint32_t)comm.rank(), (uint32_t)P, (uint64_t)P * cap_send);
   int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;

@@ -41,7 +41,6 @@ struct Knobs {
                          //   after it (1), in line (0), fused into the degree scatter (3,
                          //   graph2tree_dev; taken anyway from 2^31 records)
   int seq_compact = 1;   // SHEEP_SEQ_COMPACT: sort only the ids with degree > 0
-  int sort_radix = 0;    // SHEEP_SORT (1 = "radix"): two radix passes instead of the hi bins
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
   int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)
   int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
@@ -51,9 +50,6 @@ struct Knobs {
   int degb_plain = 1;    // SHEEP_DEGB_PLAIN: histogram adds without wave matching (bit 0: 64K
                          //   buckets, bit 1: small buckets)
   int degb_hist16 = 1;   // SHEEP_DEGB_HIST: one-read 64K-id histogram (0: two halves)
-  int bin_tm = 1;        // SHEEP_BIN_TM: tile-major count matrices
-  int bin_scatter = 1;   // SHEEP_BIN_SCATTER: unstable 16K-item bin scatter (0: stable radix scatter)
-  int ep_plain = 1;      // SHEEP_EP_PLAIN: edge pass counts bins with plain LDS atomics
   int tree_stats = 0;    // SHEEP_TREE_STATS: 1 totals, 2 per bucket (stderr; diagnostics)
   int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
   int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
@@ -62,7 +58,8 @@ struct Knobs {
                          //   first; -1 auto (from 2^27 records), 0, 1
   int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
-                         //   rank (0: every rank applies every bucket's zipper)
+                         //   rank (0: every rank applies every bucket's zipper; 2: also for
+                         //   a one-rank group, lab)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };

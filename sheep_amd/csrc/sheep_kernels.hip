@@ -333,7 +333,6 @@ __device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, ui
   }
 }
 // Tile-major count matrices and their scan (defined with the hi bins below).
-static bool bin_tile_major();
 static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
                        uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s);
 static constexpr uint32_t TM_G = 256;  // tiles per group
@@ -713,19 +712,17 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   uint32_t* stmp = offsets + cw;
   uint16_t* ep = (uint16_t*)(((uintptr_t)(stmp + degb_scan_words(cw, nchunks, NB)) + 15) & ~(uintptr_t)15);
   uint32_t H = SH > 15 ? 2u : 1u;
-  // tile-major counts (SHEEP_BIN_TM, as the hi bins): bucket starts come from the scan
-  const int tm = bin_tile_major() ? 1 : 0;
+  // tile-major counts (as the hi bins): bucket starts come from the scan
+  const int tm = 1;
   unsigned long long* bstart = nullptr;
   hipLaunchKernelGGL(k_degb_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, counts, nchunks, err, psh, yhist, tm);
   if (counted) (void)hipEventRecord(counted, s);
-  if (tm) {
+  {
     uint32_t* gsum = stmp;
     bstart = (unsigned long long*)(((uintptr_t)(gsum + NB * ((nchunks + TM_G - 1) / TM_G)) + 7) &
                                    ~(uintptr_t)7);
     tm_offsets(counts, offsets, nchunks, NB, NB, gsum, bstart, s);
-  } else {
-    launch_scan_exclusive(counts, offsets, cw, stmp, s);
   }
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
@@ -1115,15 +1112,6 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
   }
 }
 
-// Records grouped by hi bin in one pass (the hi-bin alternative to radix_sort_u64): the
-// tile histograms were counted by the edge pass (launch_edge_pass_bins).  bin_start (device,
-// nb + 1 u64) receives where each bin starts in `out`, and the total.
-__global__ void k_bin_starts(const uint32_t* __restrict__ offsets, uint32_t ntiles, uint32_t nb,
-                             uint64_t n, unsigned long long* __restrict__ bin_start) {
-  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= nb; d += gridDim.x * blockDim.x)
-    bin_start[d] = d < nb ? offsets[(uint64_t)d * ntiles] : n;
-}
-
 // Tile-major bin counts (counts[tile * 512 + bin], written by k_edge_pass_tiles<..., TM>) ->
 // tile-major global offsets, in three coalesced passes over groups of TM_G tiles:
 //   k_tm_colsum       gsum[g][bin] = records of the bin in group g;
@@ -1269,9 +1257,6 @@ k_bin_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint6
   }
 }
 
-// SHEEP_BIN_TM=0: the digit-major counts and one flat scan (the previous layout).
-static bool bin_tile_major() { return knobs().bin_tm != 0; }
-
 void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t* bins, uint32_t nb,
                   uint32_t* tmp, unsigned long long* bin_start, const uint16_t* digits,
                   hipStream_t s, unsigned long long* h_start, hipEvent_t started) {
@@ -1284,27 +1269,11 @@ void bin_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, const uint32_t*
   };
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
-  if (bin_tile_major()) {
-    if (n == 0) return;
-    tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
-    publish();
-    if (knobs().bin_scatter) {  // 0: the stable 8192-item scatter
-      hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,
-                         in, out, n, (const uint32_t*)counts, digits);
-      return;
-    }
-    hipLaunchKernelGGL((k_rsort_scatter<9, true, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in,
-                       out, n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
-    return;
-  }
-  uint32_t* stmp = tmp + 512 * nt;
-  launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
-  hipLaunchKernelGGL(k_bin_starts, dim3(3), dim3(BLOCK), 0, s, (const uint32_t*)counts, (uint32_t)nt,
-                     nb, n, bin_start);
+  if (n == 0) return;
+  tm_offsets(counts, counts, (uint32_t)nt, 512, nb, tmp + 512 * nt, bin_start, s);
   publish();
-  if (n)
-    hipLaunchKernelGGL((k_rsort_scatter<9, true>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, in, out,
-                       n, 0, (const uint32_t*)counts, (uint32_t)nt, bins, nb, digits);
+  hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)((n + BS_TILE - 1) / BS_TILE)), dim3(1024), 0, s,
+                     in, out, n, (const uint32_t*)counts, digits);
 }
 
 size_t rsort_tmp_words(uint64_t n) {
@@ -1329,7 +1298,6 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
   uint64_t nt = (n + RS_TILE - 1) / RS_TILE;
   uint32_t* counts = tmp;
   uint32_t* stmp = tmp + 512 * nt;
-  const bool tm = bin_tile_major();  // counted0: launch_edge_pass_tiles used the same layout
   unsigned long long* dstart =
       (unsigned long long*)(((uintptr_t)(stmp + 512 * ((nt + TM_G - 1) / TM_G)) + 7) & ~(uintptr_t)7);
   const uint64_t* src = in;
@@ -1341,20 +1309,16 @@ uint64_t* radix_sort_u64(const uint64_t* in, uint64_t* a, uint64_t* b, uint64_t 
       const dim3 g((unsigned)nt), bl(RS_THREADS);
       if (width > 8) {
         if (count)
-          hipLaunchKernelGGL((tm ? k_rsort_count<9, true> : k_rsort_count<9, false>), g, bl, 0, s, src, n,
-                             shift, counts, (uint32_t)nt);
-        if (tm) tm_offsets(counts, counts, (uint32_t)nt, 512, 512, stmp, dstart, s);
-        else launch_scan_exclusive(counts, counts, 512 * nt, stmp, s);
-        hipLaunchKernelGGL((tm ? k_rsort_scatter<9, false, true> : k_rsort_scatter<9, false, false>), g, bl,
+          hipLaunchKernelGGL((k_rsort_count<9, true>), g, bl, 0, s, src, n, shift, counts, (uint32_t)nt);
+        tm_offsets(counts, counts, (uint32_t)nt, 512, 512, stmp, dstart, s);
+        hipLaunchKernelGGL((k_rsort_scatter<9, false, true>), g, bl,
                            0, s, src, dst, n, shift, (const uint32_t*)counts, (uint32_t)nt,
                            (const uint32_t*)nullptr, 0u, (const uint16_t*)nullptr);
       } else {
         if (count)
-          hipLaunchKernelGGL((tm ? k_rsort_count<8, true> : k_rsort_count<8, false>), g, bl, 0, s, src, n,
-                             shift, counts, (uint32_t)nt);
-        if (tm) tm_offsets(counts, counts, (uint32_t)nt, 256, 256, stmp, dstart, s);
-        else launch_scan_exclusive(counts, counts, 256 * nt, stmp, s);
-        hipLaunchKernelGGL((tm ? k_rsort_scatter<8, false, true> : k_rsort_scatter<8, false, false>), g, bl,
+          hipLaunchKernelGGL((k_rsort_count<8, true>), g, bl, 0, s, src, n, shift, counts, (uint32_t)nt);
+        tm_offsets(counts, counts, (uint32_t)nt, 256, 256, stmp, dstart, s);
+        hipLaunchKernelGGL((k_rsort_scatter<8, false, true>), g, bl,
                            0, s, src, dst, n, shift, (const uint32_t*)counts, (uint32_t)nt,
                            (const uint32_t*)nullptr, 0u, (const uint16_t*)nullptr);
       }
@@ -1656,13 +1620,10 @@ void launch_edge_pass_bins(const uint32_t* uv, uint64_t m, const uint32_t* rank,
                            uint32_t* tmp, uint16_t* digits, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
-  const bool tm = bin_tile_major();  // every tile writes all 512 of its counts
-  if (!tm && nb < 512) (void)hipMemsetAsync(tmp + (uint64_t)nb * nt, 0, (512 - nb) * nt * 4, s);
-  auto k = tm ? (pre ? k_edge_pass_tiles<9, true, true, true> : k_edge_pass_tiles<9, false, true, true>)
-              : (pre ? k_edge_pass_tiles<9, true, true> : k_edge_pass_tiles<9, false, true>);
-  const int plain = knobs().ep_plain;  // bin counts by plain LDS atomics
+  // tile-major counts (every tile writes all 512 of its counts); bin counts by plain LDS atomics
+  auto k = pre ? k_edge_pass_tiles<9, true, true, true> : k_edge_pass_tiles<9, false, true, true>;
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
-                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits, plain);
+                     (uint32_t*)nullptr, items, err, 0, tmp, (uint32_t)nt, bins, nb, digits, 1);
 }
 
 void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
@@ -1670,11 +1631,9 @@ void launch_edge_pass_tiles(const uint32_t* uv, uint64_t m, const uint32_t* rank
                             uint32_t* tmp, hipStream_t s, bool pre) {
   if (m == 0) return;
   uint64_t nt = (m + RS_TILE - 1) / RS_TILE;
-  const bool tm = bin_tile_major();  // the layout radix_sort_u64(..., counted0) expects
-  auto k = DB > 8 ? (pre ? (tm ? k_edge_pass_tiles<9, true, false, true> : k_edge_pass_tiles<9, true>)
-                         : (tm ? k_edge_pass_tiles<9, false, false, true> : k_edge_pass_tiles<9, false>))
-                  : (pre ? (tm ? k_edge_pass_tiles<8, true, false, true> : k_edge_pass_tiles<8, true>)
-                         : (tm ? k_edge_pass_tiles<8, false, false, true> : k_edge_pass_tiles<8, false>));
+  // tile-major counts: the layout radix_sort_u64(..., counted0) expects
+  auto k = DB > 8 ? (pre ? k_edge_pass_tiles<9, true, false, true> : k_edge_pass_tiles<9, false, false, true>)
+                  : (pre ? k_edge_pass_tiles<8, true, false, true> : k_edge_pass_tiles<8, false, false, true>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, (const uint2*)uv, m, rank, n_rank,
                      pst, items, err, shift, tmp, (uint32_t)nt, (const uint32_t*)nullptr, 0u,
                      (uint16_t*)nullptr, 0);

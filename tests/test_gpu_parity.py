@@ -91,7 +91,7 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     (16, 24, 0, {"edge_part": 0}),  # direct gathers, hi bins
     (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
-    (18, 29, 0, {"bin_scatter": 0, "bin_direct": 0}),  # stable bin scatter
+    (18, 29, 0, {"bin_direct": 0}),                    # edge pass + bin scatter
     (18, 30, 0, {"part_overlap": 3}),  # fused: the degree scatter partitions the records
     (18, 32, 1, {"part_overlap": 3}),  # fused, FILE degrees
     (18, 31, 1, {"part_overlap": 0}),  # the first partition pass in line
@@ -365,7 +365,6 @@ KB_KNOBS = [
     {"kb_pipe": 0},                                  # one stream, map of bucket k after apply of k-1
     {"kb_pipe": 0, "kb_gbits": 0},
     {"kb_refresh": 0},                               # pipelined, stale kept starts zipped as they are
-    {"sort": 1},                                     # two 9-bit radix passes instead of hi bins
     {"kb_pipe": 1, "kb_buckets": 512, "kb_rankb": 512},  # many narrow buckets
     {"kb_pick": 0},                                  # the host's anchor (rank B0 - 1) for every map
     {"kb_pick": 0, "kb_pipe": 0},
