@@ -48,7 +48,7 @@ static const KnobDef kKnobs[] = {
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
-    {"ls_split", &Knobs::ls_split},
+    {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
 };
 
 static Knobs g_knobs;
@@ -964,10 +964,12 @@ struct Lockstep {
 
 // part_done (nullable): the first partition pass of the rank gathers was launched by the caller
 // into "ls_items" (with "part_ws" holding its cursors) and completes at this event.
+// nsd (nullable): the global degrees in sequence order, read instead of d_deg[d_seq[r]].
 static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
-                     uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr) {
+                     uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr,
+                     const uint32_t* nsd = nullptr) {
   require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
@@ -1020,7 +1022,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   // hi bins from the global degrees (identical on every rank)
   const size_t nch = ((size_t)n_seq + 255) / 256;
   uint64_t* cds = (uint64_t*)sc.get("ls_chunk_deg", nch * 8);
-  launch_chunk_degsum(d_seq, d_deg, n_seq, cds, s);
+  launch_chunk_degsum(d_seq, d_deg, n_seq, cds, s, nsd);
   std::vector<uint64_t> hd(nch);
   HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -1298,6 +1300,81 @@ static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t
   if (L.split) sum("kb_zip", L.zip_ev);
 }
 
+// ---- the degree sequence of P ranks, sharded (mpiSequence, sequence.h:65-93) ---------------
+// Instead of every rank sorting all ids after an all-reduce of the degrees: the degrees are
+// reduce-scattered (rank r gets the global degrees of ids [r c, (r + 1) c)), each rank sorts
+// only its ids (stable, by degree), the ranks' histograms over degree values are all-gathered,
+// and each rank computes the global position of its ids from them (launch_seq_rank; ids of
+// different ranks never interleave within a degree).  One all-gather of the rank slices gives
+// every rank the whole rank map, from which it scatters seq.  Returns n_seq; rank: n_pad
+// words (>= n_ids; INVALID for degree 0); *nsd_out: the global degrees in sequence order (for
+// the bins' estimate).  The same result as all-reduce + sequence_dev.
+static uint32_t sequence_sharded(Ctx& c, Comm& comm, const uint32_t* deg_local, uint32_t n_ids,
+                                 uint32_t* d_seq, uint32_t** rank_out, const uint32_t** nsd_out,
+                                 hipStream_t s) {
+  Scratch& sc = c.scratch;
+  const uint32_t P = (uint32_t)comm.size(), r = (uint32_t)comm.rank();
+  uint64_t cw = ((uint64_t)n_ids + P - 1) / P;
+  cw += cw & 1;  // even: the all-gathers move u64 words
+  const uint64_t n_pad = cw * P;
+  if (n_pad >= (1ull << 32)) throw ApiError(-EINVAL, "sharded sequence: id space too large");
+  const uint32_t cs = (uint32_t)cw;
+  uint32_t* send = (uint32_t*)sc.get("sq_send", n_pad * 4);
+  HIP_CHECK(hipMemcpyAsync(send, deg_local, (size_t)n_ids * 4, hipMemcpyDeviceToDevice, s));
+  if (n_pad > n_ids) HIP_CHECK(hipMemsetAsync(send + n_ids, 0, (size_t)(n_pad - n_ids) * 4, s));
+  uint32_t* dsl = (uint32_t*)sc.get("sq_slice", (size_t)cs * 4);
+  comm.reduce_scatter_sum_u32(send, dsl, cs, s);
+  uint32_t* stats = (uint32_t*)sc.get("sq_stats", 16);
+  launch_deg_stats(dsl, cs, stats, s);
+  long long* st64 = (long long*)sc.get("sq_st64", 32);
+  launch_seq_stats64(stats, cs, st64, s);
+  HIP_CHECK(hipMemcpyAsync(st64 + 2, st64 + 1, 8, hipMemcpyDeviceToDevice, s));
+  comm.allreduce_max_i64((int64_t*)st64, 1, s);           // [0] max degree over all ranks
+  comm.allreduce_sum_u64((uint64_t*)st64 + 2, 1, s);     // [2] ids of degree > 0 over all ranks
+  long long h[3];
+  HIP_CHECK(hipMemcpyAsync(h, st64, 24, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  const uint32_t maxdeg = (uint32_t)h[0], n_loc = (uint32_t)h[1];
+  const uint32_t n_seq = (uint32_t)h[2];
+  uint32_t* rank = (uint32_t*)sc.get("mt_rank", n_pad * 4);
+  *rank_out = rank;
+  *nsd_out = nullptr;
+  launch_fill(rank + (size_t)r * cs, INV, cs, s);
+  if (n_seq == 0) {
+    comm.allgather_u64((const uint64_t*)(rank + (size_t)r * cs), (uint64_t*)rank, cs / 2, s);
+    return 0;
+  }
+  const uint32_t D = maxdeg + 1, Dp = D + (D & 1);
+  // this rank's ids of degree > 0, sorted stably by degree (local ids: global - r c)
+  const int passes = (bits_for(maxdeg) + 7) / 8;
+  uint64_t* items = (uint64_t*)sc.get("seq_items", (size_t)cs * 8);
+  uint64_t* items_b = (uint64_t*)sc.get("seq_items_b", (size_t)cs * 8);
+  uint32_t* tmp = (uint32_t*)sc.get("rsort_tmp", rsort_tmp_words(cs) * 4);
+  uint32_t* ptmp = (uint32_t*)sc.get("seq_pack_tmp", pack_nz_tmp_words(cs) * 4);
+  launch_pack_nonzero(dsl, cs, items, ptmp, s);
+  const uint64_t* sorted = n_loc ? radix_sort_u64(items, items_b, items, n_loc, 0, 8 * passes, tmp, s)
+                                 : items;
+  uint32_t* H = (uint32_t*)sc.get("sq_hist", (size_t)Dp * 4);
+  uint32_t* lst = (uint32_t*)sc.get("sq_lst", (size_t)D * 4);
+  HIP_CHECK(hipMemsetAsync(H, 0, (size_t)Dp * 4, s));
+  launch_seq_runs(sorted, n_loc, lst, H, s);
+  uint32_t* hall = (uint32_t*)sc.get("sq_hall", (size_t)P * Dp * 4);
+  comm.allgather_u64((const uint64_t*)H, (uint64_t*)hall, Dp / 2, s);
+  uint32_t* tot = (uint32_t*)sc.get("sq_tot", (size_t)D * 4);
+  uint32_t* pre = (uint32_t*)sc.get("sq_pre", (size_t)D * 4);
+  uint32_t* S = (uint32_t*)sc.get("sq_S", (size_t)D * 4);
+  uint32_t* stmp = (uint32_t*)sc.get("sq_scan_tmp", scan_tmp_words(D) * 4);
+  launch_seq_base(hall, P, r, D, Dp, tot, pre, s);
+  launch_scan_exclusive(tot, S, D, stmp, s);
+  launch_seq_rank(sorted, n_loc, S, pre, lst, rank + (size_t)r * cs, s);
+  comm.allgather_u64((const uint64_t*)(rank + (size_t)r * cs), (uint64_t*)rank, cs / 2, s);
+  launch_seq_from_rank(rank, n_ids, d_seq, s);
+  uint32_t* nsd = (uint32_t*)sc.get("sq_nsd", (size_t)n_seq * 4);
+  launch_deg_of_rank(S, D, n_seq, nsd, s);
+  *nsd_out = nsd;
+  return n_seq;
+}
+
 // ---- graph2tree -i -r on one rank (the multi-GPU driver) ------------------------------------
 // This rank's shard -> its degrees, summed over the ranks (mpiSequence's MPI_Allreduce,
 // sequence.h:72-78) -> the identical seq / rank on every rank -> the lockstep tree over all
@@ -1329,15 +1406,21 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
     part_done = c.part_ev[1];
   }
-  if (n_ids) HIP_CHECK(hipMemcpyAsync(deg, deg_local, (size_t)n_ids * 4, hipMemcpyDeviceToDevice, s));
-  comm.allreduce_sum_u32(deg, n_ids, s);
-  if (tm) tm->mark("degree");
   uint32_t n_seq = n_seq_given;
-  if (!seq_given) {
-    n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
+  const uint32_t* nsd = nullptr;  // sharded: the global degrees in sequence order
+  if (!seq_given && comm.size() > 1 && knobs().ls_seq) {
+    if (tm) tm->mark("degree");
+    n_seq = sequence_sharded(c, comm, deg_local, n_ids, d_seq, &rank, &nsd, s);
   } else {
-    launch_fill(rank, INV, n_ids, s);
-    launch_rank_scatter(d_seq, n_seq, rank, c.d_err, s);
+    if (n_ids) HIP_CHECK(hipMemcpyAsync(deg, deg_local, (size_t)n_ids * 4, hipMemcpyDeviceToDevice, s));
+    comm.allreduce_sum_u32(deg, n_ids, s);
+    if (tm) tm->mark("degree");
+    if (!seq_given) {
+      n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s);
+    } else {
+      launch_fill(rank, INV, n_ids, s);
+      launch_rank_scatter(d_seq, n_seq, rank, c.d_err, s);
+    }
   }
   check_err(c, s);
   if (tm) tm->mark("sequence");
@@ -1349,7 +1432,8 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   c.ls_live++;
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
-  ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done);
+  ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done,
+           nsd);
   if (part_done) HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));  // also when no tree is built
   check_err(c, s);
   uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);

@@ -30,6 +30,7 @@ struct RcclApi {
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
@@ -49,9 +50,10 @@ static const RcclApi& rccl() {
     api.destroy = (decltype(api.destroy))dlsym(h, "ncclCommDestroy");
     api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
     api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+    api.reduce_scatter = (decltype(api.reduce_scatter))dlsym(h, "ncclReduceScatter");
     api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
     if (!api.get_unique_id || !api.init_rank || !api.destroy || !api.all_reduce ||
-        !api.all_gather || !api.error_string)
+        !api.all_gather || !api.reduce_scatter || !api.error_string)
       err = "librccl.so.1 lacks an entry point";
   });
   if (!err.empty()) throw std::runtime_error(err);
@@ -93,6 +95,9 @@ struct RcclComm : Comm {
   }
   void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override {
     nccl_check(rccl().all_gather(send, recv, n, ncclUint64, comm, s), "ncclAllGather");
+  }
+  void reduce_scatter_sum_u32(const uint32_t* send, uint32_t* recv, size_t n, hipStream_t s) override {
+    nccl_check(rccl().reduce_scatter(send, recv, n, ncclUint32, ncclSum, comm, s), "ncclReduceScatter");
   }
 };
 
@@ -188,9 +193,27 @@ struct LocalComm : Comm {
     g->ptrs[r] = send;
     g->barrier();
     for (int q = 0; q < g->P; ++q)
-      if (n) HIPC(hipMemcpyAsync(recv + (size_t)q * n, g->ptrs[q], n * 8, hipMemcpyDeviceToDevice, s));
+      if (n && (const void*)(recv + (size_t)q * n) != g->ptrs[q])
+        HIPC(hipMemcpyAsync(recv + (size_t)q * n, g->ptrs[q], n * 8, hipMemcpyDeviceToDevice, s));
     HIPC(hipStreamSynchronize(s));
     g->barrier();
+  }
+  // each rank sums its own slice of every rank's buffer (its own device pointer table)
+  void reduce_scatter_sum_u32(const uint32_t* send, uint32_t* recv, size_t n, hipStream_t s) override {
+    HIPC(hipStreamSynchronize(s));
+    g->ptrs[r] = send;
+    g->barrier();
+    if (!d_mine) HIPC(hipMalloc((void**)&d_mine, 64 * sizeof(void*)));
+    std::vector<const uint32_t*> mine(g->P);
+    for (int q = 0; q < g->P; ++q) mine[q] = (const uint32_t*)g->ptrs[q] + (size_t)r * n;
+    HIPC(hipMemcpyAsync((void*)d_mine, mine.data(), g->P * sizeof(void*), hipMemcpyHostToDevice, s));
+    launch_sum_ptrs_u32(recv, (const uint32_t* const*)d_mine, g->P, n, s);
+    HIPC(hipStreamSynchronize(s));
+    g->barrier();
+  }
+  const void** d_mine = nullptr;
+  ~LocalComm() override {
+    if (d_mine) (void)hipFree(d_mine);
   }
 };
 

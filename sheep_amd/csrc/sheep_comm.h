@@ -19,8 +19,11 @@ struct Comm {
   virtual void allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_sum_u64(uint64_t* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max_i64(int64_t* buf, size_t n, hipStream_t s) = 0;
-  // recv[r * n + i] = send_r[i]
+  // recv[r * n + i] = send_r[i]; in place when send == recv + rank * n
   virtual void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) = 0;
+  // recv[i] = sum over ranks of send_q[rank * n + i] (send: size * n elements)
+  virtual void reduce_scatter_sum_u32(const uint32_t* send, uint32_t* recv, size_t n,
+                                      hipStream_t s) = 0;
 };
 
 // RCCL (loaded with dlopen on first use: single-GPU callers never load it).  id: 128 bytes.

@@ -57,6 +57,8 @@ struct Knobs {
   int kb_gsum = -1;      // SHEEP_KB_GSUM: the map tests 64-rank "all in the giant" blocks in LDS
                          //   first; -1 auto (from 2^27 records), 0, 1
   int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
+  int ls_seq = 1;        // SHEEP_LS_SEQ: with P > 1 ranks each sorts the ids of its 1/P of the id
+                         //   space (degrees reduce-scattered; 0: all-reduced, every rank sorts all)
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
                          //   rank (0: every rank applies every bucket's zipper; 2: also for
                          //   a one-rank group, lab)
@@ -267,6 +269,15 @@ void launch_ls_zip(const uint64_t* zkept, uint32_t* zn, const uint32_t* zbm, uin
                    uint32_t B0, uint32_t B1, bool has_anchor, uint32_t* parent, uint32_t* jump,
                    hipStream_t s);
 void launch_add_u32(uint32_t* p, uint64_t n, uint32_t d, hipStream_t s);  // p[i] += d (wraps)
+// Sharded degree sequence (P > 1, sheep_capi.cpp sequence_sharded; see sheep_kernels.hip).
+void launch_seq_runs(const uint64_t* sorted, uint32_t n, uint32_t* lst, uint32_t* H, hipStream_t s);
+void launch_seq_base(const uint32_t* hall, uint32_t P, uint32_t r, uint32_t D, uint32_t Dp,
+                     uint32_t* tot, uint32_t* pre, hipStream_t s);
+void launch_seq_rank(const uint64_t* sorted, uint32_t n, const uint32_t* S, const uint32_t* pre,
+                     const uint32_t* lst, uint32_t* rank_slice, hipStream_t s);
+void launch_seq_from_rank(const uint32_t* rank, uint32_t n_ids, uint32_t* seq, hipStream_t s);
+void launch_deg_of_rank(const uint32_t* S, uint32_t D, uint32_t n_seq, uint32_t* out, hipStream_t s);
+void launch_seq_stats64(const uint32_t* stats, uint32_t c, long long* out, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
 // Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)

@@ -3232,6 +3232,108 @@ void launch_add_u32(uint32_t* p, uint64_t n, uint32_t d, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_add_u32, dim3(grid_for(n)), dim3(BLOCK), 0, s, p, n, d);
 }
 
+// ---- sharded degree sequence (multi-GPU, P > 1; sheep_capi.cpp sequence_sharded) ----------
+// Rank r holds the global degrees of ids [r c, (r + 1) c) and sorts only those, stably by
+// degree.  Ids of different ranks do not interleave, so the position in the global sequence of
+// the i-th of r's items, of degree d, is
+//   (ids of degree < d, all ranks) + (ids of degree d on ranks < r) + (i - first i of degree d)
+// and every term comes from the ranks' histograms over degree values (all-gathered).
+
+// Run bounds of each degree in the sorted local items: lst[d] = first index, H[d] = run length
+// (H zeroed; absent degrees keep H = 0 and are never read in lst).
+__global__ void k_seq_runs(const uint64_t* __restrict__ sorted, uint32_t n, uint32_t* lst,
+                           uint32_t* H) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t d = (uint32_t)(sorted[i] >> 32);
+    if (i == 0 || (uint32_t)(sorted[i - 1] >> 32) != d) {
+      lst[d] = i;
+      atomicSub(&H[d], i);
+    }
+    if (i + 1 == n || (uint32_t)(sorted[i + 1] >> 32) != d) atomicAdd(&H[d], i + 1);
+  }
+}
+
+// hall: P rows of Dp words (rank q's H).  tot[d] = ids of degree d over all ranks, pre[d] =
+// those on ranks < r.
+__global__ void k_seq_base(const uint32_t* __restrict__ hall, uint32_t P, uint32_t r, uint32_t D,
+                           uint32_t Dp, uint32_t* __restrict__ tot, uint32_t* __restrict__ pre) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < D; d += gridDim.x * blockDim.x) {
+    uint32_t t = 0, p = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+      const uint32_t h = hall[(uint64_t)q * Dp + d];
+      t += h;
+      if (q < r) p += h;
+    }
+    tot[d] = t;
+    pre[d] = p;
+  }
+}
+
+// rank_slice[local id] = global position (S: exclusive prefix of tot).
+__global__ void k_seq_rank(const uint64_t* __restrict__ sorted, uint32_t n, const uint32_t* __restrict__ S,
+                           const uint32_t* __restrict__ pre, const uint32_t* __restrict__ lst,
+                           uint32_t* __restrict__ rank_slice) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t it = sorted[i];
+    const uint32_t d = (uint32_t)(it >> 32);
+    rank_slice[(uint32_t)it] = S[d] + pre[d] + (i - lst[d]);
+  }
+}
+
+// seq[rank[v]] = v (jtree.h:165-168 the other way round).
+__global__ void k_seq_from_rank(const uint32_t* __restrict__ rank, uint32_t n_ids,
+                                uint32_t* __restrict__ seq) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_ids; v += gridDim.x * blockDim.x) {
+    const uint32_t r = rank[v];
+    if (r != INV) seq[r] = v;
+  }
+}
+
+// The global degree at every position of the sequence (non-decreasing): the largest d with
+// S[d] <= p (an absent degree has S[d] = S[d + 1], so the largest such d is present).
+__global__ void k_deg_of_rank(const uint32_t* __restrict__ S, uint32_t D, uint32_t n_seq,
+                              uint32_t* __restrict__ out) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n_seq; p += gridDim.x * blockDim.x) {
+    uint32_t lo = 1, hi = D - 1;  // S[1] = 0 <= p (degree 0 is never sorted: tot[0] = 0)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (S[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    out[p] = lo;
+  }
+}
+
+// [0] = this rank's max degree, [1] = its ids of degree > 0 (from k_deg_stats over c ids).
+__global__ void k_seq_stats64(const uint32_t* __restrict__ stats, uint32_t c, long long* out) {
+  out[0] = stats[0];
+  out[1] = (long long)(c - stats[1]);
+}
+
+void launch_seq_runs(const uint64_t* sorted, uint32_t n, uint32_t* lst, uint32_t* H, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_seq_runs, dim3(grid_for(n)), dim3(BLOCK), 0, s, sorted, n, lst, H);
+}
+void launch_seq_base(const uint32_t* hall, uint32_t P, uint32_t r, uint32_t D, uint32_t Dp,
+                     uint32_t* tot, uint32_t* pre, hipStream_t s) {
+  if (D) hipLaunchKernelGGL(k_seq_base, dim3(grid_for(D)), dim3(BLOCK), 0, s, hall, P, r, D, Dp, tot, pre);
+}
+void launch_seq_rank(const uint64_t* sorted, uint32_t n, const uint32_t* S, const uint32_t* pre,
+                     const uint32_t* lst, uint32_t* rank_slice, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_seq_rank, dim3(grid_for(n)), dim3(BLOCK), 0, s, sorted, n, S, pre, lst,
+                       rank_slice);
+}
+void launch_seq_from_rank(const uint32_t* rank, uint32_t n_ids, uint32_t* seq, hipStream_t s) {
+  if (n_ids) hipLaunchKernelGGL(k_seq_from_rank, dim3(grid_for(n_ids)), dim3(BLOCK), 0, s, rank, n_ids, seq);
+}
+void launch_deg_of_rank(const uint32_t* S, uint32_t D, uint32_t n_seq, uint32_t* out, hipStream_t s) {
+  if (n_seq && D > 1)
+    hipLaunchKernelGGL(k_deg_of_rank, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, S, D, n_seq, out);
+}
+void launch_seq_stats64(const uint32_t* stats, uint32_t c, long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_seq_stats64, dim3(1), dim3(1), 0, s, stats, c, out);
+}
+
 // ---- lockstep exchange (multi-GPU kb loop, sheep_ls_*) -----------------------------------
 // One rank's contribution to a bucket, laid out for one all-gather: `ms` u64 slots holding the
 // bucket's mark words [w0, w1] (two per slot, zero beyond w1), then `cap` kept pairs, padded

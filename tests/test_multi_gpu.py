@@ -108,7 +108,8 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
                                  {"kb_gbits": 0},                   # no giant bitmap in the maps
                                  {"kb_gsum": 1},                    # the LDS giant summary
                                  {"part_overlap": 0},               # no first pass beside the degrees
-                                 {"ls_split": 0}])                  # every rank runs every zipper
+                                 {"ls_split": 0},                   # every rank runs every zipper
+                                 {"ls_seq": 0}])                    # every rank sorts all ids
 def test_multi_local_front_half_options(oracle, gpu, options, env):
     """The multi-rank driver under the front-half / anchor options: the same tree (R-MAT 19,
     P = 2: 2^22 records per rank, so each rank runs the partitioned gathers)."""
