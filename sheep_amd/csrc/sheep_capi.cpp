@@ -914,6 +914,9 @@ struct Lockstep {
   // only for a one-rank group: with P ranks the refresh would repeat on every rank the finds
   // that the maps split P ways.
   bool defer = false;
+  // per-bucket apply spans ("kb_apply": the one-GPU rehearsal's per-rank apply time); the
+  // multi-GPU driver times only the maps
+  bool time_apply = true;
   // Split apply (P > 1 ranks, launch_ls_fold_union_label / launch_ls_zip): bucket k's spine and
   // zipper run only on its owner rank (k mod P), on zs, from copies of the bucket's refreshed
   // pairs and marks (two slots, by owned-bucket parity); every rank applies the union-find part.
@@ -1019,18 +1022,22 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     counts_out[0] = m;
     return;
   }
-  // hi bins from the global degrees (identical on every rank)
+  // hi bins from the global degrees (identical on every rank): the chunk sums go to pinned host
+  // memory, and the host cuts the bins while the second partition pass (which needs no bins)
+  // runs
+  Ctx& c = *L.ctx;
   const size_t nch = ((size_t)n_seq + 255) / 256;
   uint64_t* cds = (uint64_t*)sc.get("ls_chunk_deg", nch * 8);
   launch_chunk_degsum(d_seq, d_deg, n_seq, cds, s, nsd);
-  std::vector<uint64_t> hd(nch);
-  HIP_CHECK(hipMemcpyAsync(hd.data(), cds, nch * 8, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  std::vector<double> est;
-  L.bounds = make_bins(hd, n_seq, &est);
-  const uint32_t nb = (uint32_t)L.bounds.size();
-  L.bins = (uint32_t*)sc.get("ls_bins", 512 * 4);
-  HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
+  if (c.h_chunks_n < nch) {
+    if (c.h_chunks) HIP_CHECK(hipHostFree(c.h_chunks));
+    c.h_chunks = nullptr;
+    c.h_chunks_n = 0;
+    HIP_CHECK(hipHostMalloc((void**)&c.h_chunks, nch * 8, hipHostMallocDefault));
+    c.h_chunks_n = nch;
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_chunks, cds, nch * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipEventRecord(c.bins_ev, s));
   // this shard's records -> items (hi, lo) grouped by bin
   const uint64_t mm = std::max<uint64_t>(m, 1);
   uint64_t* items = (uint64_t*)sc.get("ls_items", mm * 8);
@@ -1050,6 +1057,13 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     }
     src = (const uint32_t*)items_b;
   }
+  HIP_CHECK(hipEventSynchronize(c.bins_ev));
+  std::vector<uint64_t> hd(c.h_chunks, c.h_chunks + nch);
+  std::vector<double> est;
+  L.bounds = make_bins(hd, n_seq, &est);
+  const uint32_t nb = (uint32_t)L.bounds.size();
+  L.bins = (uint32_t*)sc.get("ls_bins", 512 * 4);
+  HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
   // Direct binning, as the one-GPU path: this shard's share of each bin's estimate (the bins
   // and estimates are global) sizes its capacity; a bin that outgrows it sends this rank
   // through the scatter below (ranks may differ in that: only per-bin counts are exchanged).
@@ -1196,20 +1210,29 @@ static void ls_pack(Lockstep& L, uint32_t k, uint64_t* d_send, uint32_t cap, hip
   launch_ls_pack(L.bm_of(k), w0, w1, L.ms, d_send, L.cnt_of(k) + 3, cap, s);
 }
 
+// solo (a group of one, nothing exchanged): d_recv is the map's own output buffer of bucket k
+// (its kept pairs at d_recv + S, their count and the marks where the map left them), applied
+// in place; cap is ignored.
 static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P, uint32_t cap,
-                     hipStream_t s) {
+                     hipStream_t s, bool solo = false) {
   if (k >= L.global_e.size()) throw ApiError(-EINVAL, "lockstep: bucket index out of range");
   const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
   uint32_t w0, w1;
   ls_words(L, k, &w0, &w1);
-  // a larger kept buffer replaces one that earlier applies may still read: drain first
-  const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
-  if (L.kept_bytes == 0) L.kept_bytes = L.scp->bytes_of("ls_kept_all");
-  if (need > L.kept_bytes) {
-    HIP_CHECK(hipDeviceSynchronize());
-    L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
+  uint64_t* kept = nullptr;
+  if (solo) {
+    kept = (uint64_t*)d_recv + L.ms;
+  } else {
+    // a larger kept buffer replaces one that earlier applies may still read: drain first
+    const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
+    if (L.kept_bytes == 0) L.kept_bytes = L.scp->bytes_of("ls_kept_all");
+    if (need > L.kept_bytes) {
+      HIP_CHECK(hipDeviceSynchronize());
+      L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
+    }
+    kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
   }
-  uint64_t* kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
+  const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
   // the anchor of map k+1 first: the union-find is as bucket k-1 left it (the caller applies
   // in order on one stream and has waited for map k), and map k+1 waits for this pick
   size_t gslot = k;  // the bitmap slot most recently written on this stream
@@ -1223,7 +1246,8 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     HIP_CHECK(hipEventRecord(L.pick_ev[(k + 1) & 1], s));
     gslot = k + 1;
   }
-  auto ev = L.span(L.apply_ev, s);
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (L.time_apply) ev = L.span(L.apply_ev, s);
   if (L.split) {
     // Every rank: the marks (OR over ranks), the fold, the union of the pairs read straight
     // from d_recv (their starts need no refresh for that), the labels.  The bucket's owner
@@ -1260,30 +1284,40 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     launch_ls_fold_union_label(ne, B0, B1, L.anchor(k), L.uf, L.label, d_recv, P, L.ms, cap,
                                L.bm_of(k), L.cnt_of(k), L.gbits, gx, s, anc_k,
                                L.anc ? L.anc + ((k + 1) & 1) : nullptr);
-    HIP_CHECK(hipEventRecord(ev.second, s));
+    if (ev.second) HIP_CHECK(hipEventRecord(ev.second, s));
     return;
   }
-  launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
+  if (!solo) launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
   launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
                   L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, L.gbits,
                   L.gbits ? L.gx + (gslot & 1) : nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
                   L.anc ? L.anc + ((k + 1) & 1) : nullptr);
-  HIP_CHECK(hipEventRecord(ev.second, s));
+  if (ev.second) HIP_CHECK(hipEventRecord(ev.second, s));
 }
 
+// The session's kernel-span sums (after its work has completed) -> c.timings.
+static void ls_timings(Ctx& c, Lockstep& L);
+
+// sync = false: only enqueued (the caller synchronises, then calls ls_timings).
 static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t* d_deg,
                       const uint32_t* d_selfc, int mode, uint32_t* d_parent, uint32_t* d_pst,
-                      hipStream_t s) {
+                      hipStream_t s, bool sync = true) {
   for (int z = 0; z < 2; ++z)  // split: this rank's zippers
     if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));
   if (L.n_seq) {
     launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
     HIP_CHECK(hipMemcpyAsync(d_parent, L.parent, (size_t)L.n_seq * 4, hipMemcpyDeviceToDevice, s));
   }
+  if (!sync) return;
   HIP_CHECK(hipStreamSynchronize(s));
+  ls_timings(c, L);
+}
+
+static void ls_timings(Ctx& c, Lockstep& L) {
   c.timings.clear();
   c.span_names.clear();
   auto sum = [&](const char* name, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+    if (v.empty()) return;
     double t = 0;
     for (auto& e : v) {
       float ms = 0;
@@ -1429,6 +1463,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   L.ctx = &c;
   L.scp = &c.scratch;
   L.defer = comm.size() == 1 && knobs().kb_defer != 0;
+  L.time_apply = false;
   c.ls_live++;
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
@@ -1475,7 +1510,16 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;
   hipEvent_t* applied = c.kb_ev + 2;
+  // A group of one exchanges nothing: each map writes into recv[k & 1] (its kept pairs are
+  // then where the apply reads them) and no count travels to the host.
+  const bool solo = P == 1 && !L.split;
   auto produce = [&](uint32_t k) {
+    const int p = k & 1;
+    if (solo) {
+      ls_map(L, k, recv[p], nullptr, nullptr, s2);
+      HIP_CHECK(hipEventRecord(exchanged[p], s2));
+      return;
+    }
     ls_map(L, k, send, (long long*)d_cnt, nullptr, s2);
     comm.allreduce_max_i64(d_cnt, 1, s2);
     HIP_CHECK(hipMemcpyAsync(c.h_pinned, d_cnt, 8, hipMemcpyDeviceToHost, s2));
@@ -1484,7 +1528,6 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     const uint64_t width = (uint64_t)S + cap;
     if (width > cap_send) throw ApiError(-EIO, "lockstep: kept pairs exceed the bucket's records");
     ls_pack(L, k, send, cap, s2);
-    const int p = k & 1;
     comm.allgather_u64(send, recv[p], width, s2);
     HIP_CHECK(hipEventRecord(exchanged[p], s2));
     caps[p] = cap;
@@ -1495,7 +1538,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     produce(0);
     for (uint32_t k = 0; k < nbk; ++k) {
       HIP_CHECK(hipStreamWaitEvent(s, exchanged[k & 1], 0));
-      ls_apply(L, k, recv[k & 1], (uint32_t)P, caps[k & 1], s);
+      ls_apply(L, k, recv[k & 1], (uint32_t)P, caps[k & 1], s, solo);
       HIP_CHECK(hipEventRecord(applied[k & 1], s));
       if (k + 1 < nbk) {
         if (k >= 1) HIP_CHECK(hipStreamWaitEvent(s2, applied[(k + 1) & 1], 0));
@@ -1504,15 +1547,16 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     }
   }
   if (tm) tm->mark("tree");
-  ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, d_pst, s);
+  ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, d_pst, s, false);
   if (L.split) {  // the owners' forests are disjoint: sum parent + 1 (INVALID + 1 = 0)
     launch_add_u32(d_parent, n_seq, 1u, s);
     comm.allreduce_sum_u32(d_parent, n_seq, s);
     launch_add_u32(d_parent, n_seq, INV, s);
   }
-  comm.allreduce_sum_u32(d_pst, n_seq, s);
-  HIP_CHECK(hipStreamSynchronize(s));
+  if (P > 1) comm.allreduce_sum_u32(d_pst, n_seq, s);
   if (tm) tm->mark("pst");
+  HIP_CHECK(hipStreamSynchronize(s));
+  ls_timings(c, L);
   return n_seq;
 }
 
