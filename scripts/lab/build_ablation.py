@@ -254,6 +254,8 @@ void launch_edge_bin(""")],
   constexpr int V = 4;
   if (bstart && (s1 - s0) * NB > 4 * bstart[NB]) plain = 0;  // a run 4x the mean: a hub's
   for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {""")],
+    # first partition pass by 512 / 2048 y digits (512 KB / 128 KB rank slices; correct results)
+    "py512": [("static constexpr uint32_t PD_Y = 1024,", "static constexpr uint32_t PD_Y = 512,")],
     "eb1024x4": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 4;")],
     "eb1024x6": [("  constexpr int NT = 1024, IT = 8;", "  constexpr int NT = 1024, IT = 6;")],
 }

@@ -1117,8 +1117,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
 // The split apply for rank `rank` of P (P > 1; after ls_begin).  Its own buffers are taken from
 // the session's scratch; kept_hint: the largest P * cap the loop will apply (0: grown on demand).
 static void ls_set_split(Lockstep& L, uint32_t rank, uint32_t P, uint64_t kept_hint) {
-  if ((P < 2 && knobs().ls_split != 2) || rank >= P)
-    throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
+  if (P < 2 || rank >= P) throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
   Scratch& sc = *L.scp;
   L.split = true;
   L.rank = rank;
@@ -1219,12 +1218,12 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   const uint32_t B0 = L.bk[k].first, B1 = L.bk[k + 1].first;
   uint32_t w0, w1;
   ls_words(L, k, &w0, &w1);
-  uint64_t* kept = nullptr;
+  const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;  // the unpacked pairs
+  uint64_t* kept = nullptr;  // where the replicated apply reads the pairs (not split)
   if (solo) {
     kept = (uint64_t*)d_recv + L.ms;
-  } else {
+  } else if (!L.split) {
     // a larger kept buffer replaces one that earlier applies may still read: drain first
-    const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
     if (L.kept_bytes == 0) L.kept_bytes = L.scp->bytes_of("ls_kept_all");
     if (need > L.kept_bytes) {
       HIP_CHECK(hipDeviceSynchronize());
@@ -1232,7 +1231,6 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     }
     kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
   }
-  const size_t need = std::max<uint64_t>((uint64_t)P * cap, 1) * 8;
   // the anchor of map k+1 first: the union-find is as bucket k-1 left it (the caller applies
   // in order on one stream and has waited for map k), and map k+1 waits for this pick
   size_t gslot = k;  // the bitmap slot most recently written on this stream
@@ -1502,10 +1500,11 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   uint64_t* send = (uint64_t*)c.scratch.get("mt_send", cap_send * 8);
   uint64_t* recv[2] = {(uint64_t*)c.scratch.get("mt_recv0", (uint64_t)P * cap_send * 8),
                        (uint64_t*)c.scratch.get("mt_recv1", (uint64_t)P * cap_send * 8)};
-  (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);  // ls_apply's unpacked pairs
   L.kept_bytes = 0;
-  if (((P > 1 && knobs().ls_split) || knobs().ls_split == 2) && n_seq)  // 2: also one rank (lab)
+  if (P > 1 && knobs().ls_split && n_seq)
     ls_set_split(L, (uint32_t)comm.rank(), (uint32_t)P, (uint64_t)P * cap_send);
+  if (!L.split && P > 1)  // ls_apply's unpacked pairs, sized once
+    (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);
   int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;

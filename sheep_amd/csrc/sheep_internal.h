@@ -60,8 +60,7 @@ struct Knobs {
   int ls_seq = 1;        // SHEEP_LS_SEQ: with P > 1 ranks each sorts the ids of its 1/P of the id
                          //   space (degrees reduce-scattered; 0: all-reduced, every rank sorts all)
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
-                         //   rank (0: every rank applies every bucket's zipper; 2: also for
-                         //   a one-rank group, lab)
+                         //   rank (0: every rank applies every bucket's zipper)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
