@@ -82,8 +82,8 @@ int sheep_abi_version(void);
  * kernels and never change a result.  Their defaults come from SHEEP_<NAME> environment
  * variables, read ONCE when the library first initialises a device; afterwards only these
  * calls change them (process-wide).  Names: degree, edge_part, part_overlap, seq_compact,
- * sort, kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, kb_defer, degb_plain, degb_hist, bin_tm,
- * bin_scatter, ep_plain, tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum, eval_pass.
+ * kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, kb_defer, degb_plain, degb_hist,
+ * tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum, eval_pass, ls_split, ls_seq.
  * -EINVAL for an unknown name. */
 int sheep_set_option(const char* name, long long value);
 int sheep_get_option(const char* name, long long* value);
@@ -221,6 +221,11 @@ int sheep_ls_free(void* handle);
 #define SHEEP_COMM_ID_BYTES 128
 int sheep_comm_unique_id(uint8_t* id_out);
 int sheep_comm_init(const uint8_t* id, int n_ranks, int rank);
+/* The same group through host shared memory instead of RCCL (name: a POSIX shm name "/..."
+ * that every rank passes; rank 0 creates it): the collectives are staged on the host, so P
+ * processes can share one GPU.  For rehearsing the multi-process driver where RCCL cannot run
+ * (it refuses two ranks on one device); not a transport for real runs. */
+int sheep_comm_init_host(const char* name, int n_ranks, int rank);
 int sheep_comm_free(void);
 int sheep_comm_info(int* rank, int* n_ranks);
 

@@ -86,6 +86,7 @@ def lib():
         "sheep_ls_free": [vp],
         "sheep_comm_unique_id": [vp],
         "sheep_comm_init": [vp, c.c_int, c.c_int],
+        "sheep_comm_init_host": [c.c_char_p, c.c_int, c.c_int],
         "sheep_comm_free": [],
         "sheep_comm_info": [vp, vp],
         "sheep_mpi_sequence": [u32p, c.c_uint64, c.c_uint32, c.c_int, u32p, c.c_uint32, u32p],

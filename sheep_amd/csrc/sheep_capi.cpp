@@ -2205,6 +2205,16 @@ int sheep_comm_init(const uint8_t* id, int n_ranks, int rank) {
   API_END
 }
 
+int sheep_comm_init_host(const char* name, int n_ranks, int rank) {
+  API_BEGIN
+  if (!name || name[0] != '/' || n_ranks < 1 || rank < 0 || rank >= n_ranks)
+    throw ApiError(-EINVAL, "comm: name (\"/...\"), n_ranks, rank");
+  Ctx& c = ctx();
+  if (c.comm) throw ApiError(-EBUSY, "comm: this device already has a communicator");
+  c.comm = shm_comm(name, n_ranks, rank, 16ull << 20).release();
+  API_END
+}
+
 int sheep_comm_free(void) {
   API_BEGIN
   Ctx& c = ctx();

@@ -3,6 +3,15 @@
 // MPI_Allreduce MAX / SUM of the degrees (sequence.h:72,78) and the MPI_Reduce of the trees
 // (jnode.cpp:241), here an all-gather of each bucket's kept pairs and a sum of pst_weight.
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <thread>
 
 #include <condition_variable>
 #include <cstring>
@@ -219,6 +228,154 @@ struct LocalComm : Comm {
 
 std::unique_ptr<Comm> local_comm(std::shared_ptr<LocalGroup> g, int rank) {
   return std::unique_ptr<Comm>(new LocalComm(std::move(g), rank));
+}
+
+// ---- P processes through host shared memory -------------------------------------------------
+// The rehearsal of the multi-process driver where RCCL cannot run (every process on the one GPU
+// of a test box): each rank stages its buffer in its slot of a POSIX shared-memory region, a
+// process-shared barrier orders the ranks, and each rank combines the slots on the host.
+// Synchronous (the stream is drained first), chunked by the slot size.  Tests only: the bytes
+// cross PCIe twice.
+struct ShmHeader {
+  pthread_barrier_t bar;
+  std::atomic<uint32_t> ready;
+  uint32_t n_ranks;
+  uint64_t slot_bytes;
+};
+static constexpr uint32_t SHM_MAGIC = 0x5ee95ee9u;
+static constexpr size_t SHM_HDR = 4096;
+
+struct ShmComm : Comm {
+  int r = 0, p = 1;
+  std::string name;
+  size_t bytes = 0;
+  ShmHeader* hdr = nullptr;
+  char* slots = nullptr;
+  uint64_t slot = 0;
+  std::vector<char> tmp;
+  ShmComm(const char* nm, int n_ranks, int rank, uint64_t slot_bytes) : r(rank), p(n_ranks), name(nm) {
+    slot = slot_bytes;
+    bytes = SHM_HDR + (size_t)p * slot;
+    int fd = -1;
+    if (r == 0) {
+      shm_unlink(name.c_str());  // a stale region of a crashed run
+      fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) throw std::runtime_error("shm: create " + name);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        fd = shm_open(name.c_str(), O_RDWR, 0600);
+        struct stat st;
+        if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size >= bytes) break;
+        if (fd >= 0) close(fd);
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+          throw std::runtime_error("shm: no region " + name);
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+    }
+    void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (base == MAP_FAILED) throw std::runtime_error("shm: mmap " + name);
+    hdr = (ShmHeader*)base;
+    slots = (char*)base + SHM_HDR;
+    if (r == 0) {
+      pthread_barrierattr_t a;
+      pthread_barrierattr_init(&a);
+      pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+      pthread_barrier_init(&hdr->bar, &a, (unsigned)p);
+      pthread_barrierattr_destroy(&a);
+      hdr->n_ranks = (uint32_t)p;
+      hdr->slot_bytes = slot;
+      hdr->ready.store(SHM_MAGIC, std::memory_order_release);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hdr->ready.load(std::memory_order_acquire) != SHM_MAGIC) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+          throw std::runtime_error("shm: region never initialised");
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      if (hdr->n_ranks != (uint32_t)p || hdr->slot_bytes != slot)
+        throw std::runtime_error("shm: ranks disagree on the group");
+    }
+    barrier();
+    if (r == 0) shm_unlink(name.c_str());  // every rank is attached: the name can go
+  }
+  ~ShmComm() override {
+    if (hdr) munmap((void*)hdr, bytes);
+  }
+  void barrier() { pthread_barrier_wait(&hdr->bar); }
+  char* slot_of(int q) const { return slots + (size_t)q * slot; }
+  int rank() const override { return r; }
+  int size() const override { return p; }
+
+  // out[i] = op over ranks of in_q[i] (in: device, each rank's own); chunked by the slot size
+  template <typename T, typename OP>
+  void reduce_to(const T* in, T* out, size_t n, hipStream_t s, OP op) {
+    const size_t per = slot / sizeof(T);
+    tmp.resize(std::min(n, per) * sizeof(T));
+    T* acc = (T*)tmp.data();
+    HIPC(hipStreamSynchronize(s));
+    for (size_t off = 0; off < n; off += per) {
+      const size_t c = std::min(per, n - off);
+      HIPC(hipMemcpy(slot_of(r), in + off, c * sizeof(T), hipMemcpyDeviceToHost));
+      barrier();
+      memcpy(acc, slot_of(0), c * sizeof(T));
+      for (int q = 1; q < p; ++q) {
+        const T* x = (const T*)slot_of(q);
+        for (size_t i = 0; i < c; ++i) acc[i] = op(acc[i], x[i]);
+      }
+      barrier();
+      HIPC(hipMemcpy(out + off, acc, c * sizeof(T), hipMemcpyHostToDevice));
+    }
+  }
+  void allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+    reduce_to(buf, buf, n, s, [](uint32_t a, uint32_t b) { return a + b; });
+  }
+  void allreduce_sum_u64(uint64_t* buf, size_t n, hipStream_t s) override {
+    reduce_to(buf, buf, n, s, [](uint64_t a, uint64_t b) { return a + b; });
+  }
+  void allreduce_max_i64(int64_t* buf, size_t n, hipStream_t s) override {
+    reduce_to(buf, buf, n, s, [](int64_t a, int64_t b) { return a > b ? a : b; });
+  }
+  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override {
+    const size_t per = slot / 8;
+    HIPC(hipStreamSynchronize(s));
+    for (size_t off = 0; off < n; off += per) {
+      const size_t c = std::min(per, n - off);
+      HIPC(hipMemcpy(slot_of(r), send + off, c * 8, hipMemcpyDeviceToHost));
+      barrier();
+      for (int q = 0; q < p; ++q)
+        HIPC(hipMemcpy(recv + (size_t)q * n + off, slot_of(q), c * 8, hipMemcpyHostToDevice));
+      barrier();
+    }
+  }
+  void reduce_scatter_sum_u32(const uint32_t* send, uint32_t* recv, size_t n, hipStream_t s) override {
+    // rank q's slice is the sum of every rank's send[q n, q n + n): one reduction per slice,
+    // each rank keeping its own
+    for (int q = 0; q < p; ++q) {
+      std::vector<uint32_t> part;
+      const size_t per = slot / 4;
+      HIPC(hipStreamSynchronize(s));
+      for (size_t off = 0; off < n; off += per) {
+        const size_t c = std::min(per, n - off);
+        HIPC(hipMemcpy(slot_of(r), send + (size_t)q * n + off, c * 4, hipMemcpyDeviceToHost));
+        barrier();
+        if (q == r) {
+          part.assign((const uint32_t*)slot_of(0), (const uint32_t*)slot_of(0) + c);
+          for (int u = 1; u < p; ++u) {
+            const uint32_t* x = (const uint32_t*)slot_of(u);
+            for (size_t i = 0; i < c; ++i) part[i] += x[i];
+          }
+          HIPC(hipMemcpy(recv + off, part.data(), c * 4, hipMemcpyHostToDevice));
+        }
+        barrier();
+      }
+    }
+  }
+};
+
+std::unique_ptr<Comm> shm_comm(const char* name, int n_ranks, int rank, uint64_t slot_bytes) {
+  return std::unique_ptr<Comm>(new ShmComm(name, n_ranks, rank, slot_bytes));
 }
 
 }  // namespace sheep

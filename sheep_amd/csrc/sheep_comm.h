@@ -30,6 +30,11 @@ struct Comm {
 void rccl_unique_id(uint8_t* id);
 std::unique_ptr<Comm> rccl_comm(const uint8_t* id, int n_ranks, int rank);
 
+// P processes through POSIX shared memory (name: "/..."), collectives staged on the host: the
+// multi-process rehearsal on a one-GPU box (tests).  Rank 0 creates the region; the others
+// attach within 60 s.
+std::unique_ptr<Comm> shm_comm(const char* name, int n_ranks, int rank, uint64_t slot_bytes);
+
 // P ranks as P threads of one process on one device: the collectives become device copies
 // and a sum / max kernel between barriers.  make_local_group returns the shared state; each
 // thread then takes local_comm(group, rank).

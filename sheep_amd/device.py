@@ -215,6 +215,11 @@ def comm_init(uid, n_ranks, rank):
     capi.call("sheep_comm_init", ctypes.cast(buf, ctypes.c_void_p), int(n_ranks), int(rank))
 
 
+def comm_init_host(name, n_ranks, rank):
+    """The group through host shared memory (sheep_comm_init_host): P processes on one GPU."""
+    capi.call("sheep_comm_init_host", name.encode(), int(n_ranks), int(rank))
+
+
 def comm_free():
     capi.call("sheep_comm_free")
 

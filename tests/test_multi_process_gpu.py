@@ -1,0 +1,74 @@
+"""The multi-GPU driver (sheep_graph2tree_multi_dev, the code bench.py and `graph2tree -i -r`
+run on every rank of an 8-GPU job) as P separate processes, the way torchrun / mpirun launch it.
+
+RCCL refuses two ranks on one device, so on a one-GPU box the processes share cuda:0 and join
+through the host shared-memory communicator (sheep_comm_init_host): the same C++ driver, each
+process with its own HIP context and its own scratch, the collectives staged on the host.  It
+covers what the P-thread rehearsal (test_multi_gpu.py) cannot: per-process state, the
+all-gather and reduce-scatter layouts across processes, and every rank's copy of the result.
+Bit-exact against the CPU checker."""
+import uuid
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _u32(t, n):
+    return t[:n].cpu().numpy().view(np.uint32).copy()
+
+
+def _rank(r, world, name, scale, seed, opts, q):
+    try:
+        import torch
+
+        from sheep_amd import capi, device
+        from sheep_amd.dist import shard_bounds
+
+        device.init(0)
+        for k, v in opts.items():
+            capi.set_option(k, v)
+        m = 16 << scale
+        lo, hi = shard_bounds(m, r, world)
+        uv = device.rmat(scale, 16, seed, lo, hi)
+        torch.cuda.synchronize()
+        device.comm_init_host(name, world, r)
+        try:
+            seq, parent, pst, n = device.graph2tree_multi(uv, 1 << scale)
+            torch.cuda.synchronize()
+            q.put((r, n, _u32(seq, n), _u32(parent, n), _u32(pst, n), None))
+        finally:
+            device.comm_free()
+    except Exception as e:  # reported to the parent (a failing rank leaves the others waiting)
+        q.put((r, 0, None, None, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,scale,seed,opts", [
+    (2, 16, 41, {}),
+    (3, 17, 42, {}),                              # three ranks: uneven id slices
+    (4, 16, 43, {"ls_split": 0, "ls_seq": 0}),    # replicated apply, all-reduced degrees
+])
+def test_multi_process_host_comm(oracle, world, scale, seed, opts):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = "/sheep-test-%s" % uuid.uuid4().hex[:16]
+    pc = mp.start_processes(_rank, args=(world, name, scale, seed, opts, q), nprocs=world,
+                            join=False, start_method="spawn")
+    got = {}
+    for _ in range(world):
+        r, n, seq, parent, pst, err = q.get(timeout=240)
+        assert err is None, "rank %d: %s" % (r, err)
+        got[r] = (n, seq, parent, pst)
+    while not pc.join(timeout=60):
+        pass
+    uv = oracle.rmat(scale, 16, seed)
+    oseq = oracle.degree_sequence(uv)
+    p, s = oracle.build_tree(uv, oseq)
+    for r in range(world):  # every rank holds the whole tree
+        n, seq, parent, pst = got[r]
+        assert n == oseq.size
+        assert np.array_equal(seq, oseq)
+        assert np.array_equal(parent, p)
+        assert np.array_equal(pst, s)
