@@ -1297,13 +1297,14 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
 static void ls_timings(Ctx& c, Lockstep& L);
 
 // sync = false: only enqueued (the caller synchronises, then calls ls_timings).
+// d_pst nullable: pst already computed (multi_tree does it beside the last applies).
 static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t* d_deg,
                       const uint32_t* d_selfc, int mode, uint32_t* d_parent, uint32_t* d_pst,
                       hipStream_t s, bool sync = true) {
   for (int z = 0; z < 2; ++z)  // split: this rank's zippers
     if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));
   if (L.n_seq) {
-    launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
+    if (d_pst) launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
     HIP_CHECK(hipMemcpyAsync(d_parent, L.parent, (size_t)L.n_seq * 4, hipMemcpyDeviceToDevice, s));
   }
   if (!sync) return;
@@ -1531,9 +1532,9 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     HIP_CHECK(hipEventRecord(exchanged[p], s2));
     caps[p] = cap;
   };
+  HIP_CHECK(hipEventRecord(c.kb_ev[4], s));  // s2 starts after everything before the loop
+  HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
   if (nbk) {
-    HIP_CHECK(hipEventRecord(c.kb_ev[4], s));
-    HIP_CHECK(hipStreamWaitEvent(s2, c.kb_ev[4], 0));
     produce(0);
     for (uint32_t k = 0; k < nbk; ++k) {
       HIP_CHECK(hipStreamWaitEvent(s, exchanged[k & 1], 0));
@@ -1545,14 +1546,22 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
       }
     }
   }
+  // pst needs only the maps' hi counts: it is computed and summed over the ranks on the map
+  // stream, beside the last applies and zippers; the parent sum then waits for it (one
+  // collective at a time on the communicator, in the same order on every rank)
+  if (n_seq) {
+    launch_pst_from_count(d_seq, n_seq, deg_local, selfc, mode, L.hcnt, d_pst, s2);
+    if (P > 1) comm.allreduce_sum_u32(d_pst, n_seq, s2);
+  }
+  HIP_CHECK(hipEventRecord(c.kb_ev[4], s2));
   if (tm) tm->mark("tree");
-  ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, d_pst, s, false);
+  ls_finish(c, L, d_seq, deg_local, selfc, mode, d_parent, nullptr, s, false);
+  HIP_CHECK(hipStreamWaitEvent(s, c.kb_ev[4], 0));
   if (L.split) {  // the owners' forests are disjoint: sum parent + 1 (INVALID + 1 = 0)
     launch_add_u32(d_parent, n_seq, 1u, s);
     comm.allreduce_sum_u32(d_parent, n_seq, s);
     launch_add_u32(d_parent, n_seq, INV, s);
   }
-  if (P > 1) comm.allreduce_sum_u32(d_pst, n_seq, s);
   if (tm) tm->mark("pst");
   HIP_CHECK(hipStreamSynchronize(s));
   ls_timings(c, L);
