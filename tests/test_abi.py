@@ -45,7 +45,20 @@ def test_lockstep_entry_points_reject_null_handles_without_gpu():
     counts = (ctypes.c_uint64 * 4)()
     assert L.sheep_ls_plan(None, counts, ctypes.byref(n), ctypes.byref(n)) == -errno.EINVAL
     assert b"null" in L.sheep_last_error()
+    assert L.sheep_ls_split(None, 0, 2) == -errno.EINVAL
     assert L.sheep_ls_free(None) == 0
+
+
+def test_host_comm_rejects_bad_arguments_without_gpu():
+    """sheep_comm_init_host checks its name and ranks before touching a device or shared
+    memory (the multi-process rehearsal's communicator)."""
+    import errno
+
+    L = capi.lib()
+    assert "sheep_comm_init_host" in capi.header_symbols()
+    assert L.sheep_comm_init_host(b"no-slash", 2, 0) == -errno.EINVAL
+    assert L.sheep_comm_init_host(b"/sheep-x", 2, 2) == -errno.EINVAL
+    assert L.sheep_comm_init_host(None, 2, 0) == -errno.EINVAL
 
 
 def test_options_read_once_and_settable_without_gpu():
@@ -55,5 +68,11 @@ def test_options_read_once_and_settable_without_gpu():
 
     old = capi.set_option("kb_buckets", 7)
     assert capi.set_option("kb_buckets", old) == 7
+    for name in ("ls_split", "ls_seq"):  # the multi-rank driver's options
+        v = capi.set_option(name, 0)
+        assert capi.set_option(name, v) == 0
+    for gone in ("sort", "bin_tm", "bin_scatter", "ep_plain"):  # A/B paths removed in round 3
+        with pytest.raises(capi.SheepError):
+            capi.set_option(gone, 0)
     with pytest.raises(capi.SheepError):
         capi.set_option("no_such_option", 1)
