@@ -57,12 +57,17 @@ def test_multi_process_host_comm(oracle, world, scale, seed, opts):
     pc = mp.start_processes(_rank, args=(world, name, scale, seed, opts, q), nprocs=world,
                             join=False, start_method="spawn")
     got = {}
-    for _ in range(world):
-        r, n, seq, parent, pst, err = q.get(timeout=240)
-        assert err is None, "rank %d: %s" % (r, err)
-        got[r] = (n, seq, parent, pst)
-    while not pc.join(timeout=60):
-        pass
+    try:
+        for _ in range(world):
+            r, n, seq, parent, pst, err = q.get(timeout=240)
+            assert err is None, "rank %d: %s" % (r, err)
+            got[r] = (n, seq, parent, pst)
+        while not pc.join(timeout=60):
+            pass
+    finally:  # a failed rank leaves the others in a barrier: end them, not the run
+        for proc in pc.processes:
+            if proc.is_alive():
+                proc.kill()
     uv = oracle.rmat(scale, 16, seed)
     oseq = oracle.degree_sequence(uv)
     p, s = oracle.build_tree(uv, oseq)
