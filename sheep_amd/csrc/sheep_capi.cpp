@@ -38,7 +38,7 @@ struct KnobDef {
 };
 static const KnobDef kKnobs[] = {
     {"degree", &Knobs::degree},           {"edge_part", &Knobs::edge_part},
-    {"part_overlap", &Knobs::part_overlap}, {"seq_compact", &Knobs::seq_compact},
+    {"part_overlap", &Knobs::part_overlap}, {"seq_sort", &Knobs::seq_sort},
     {"kb_buckets", &Knobs::kb_buckets},
     {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
     {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},
@@ -352,13 +352,32 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   HIP_CHECK(hipStreamSynchronize(s));
   uint32_t maxdeg = c.h_pinned[0], zeros = c.h_pinned[1];
   uint32_t n_seq = n_ids - zeros;
+  if (n_seq == 0) {
+    if (d_rank) launch_fill(d_rank, INV, n_ids, s);
+    return 0;
+  }
+  if (knobs().seq_sort == 2) {  // counting sort by degree; radix only for degrees >= 1024
+    uint32_t* qtmp = (uint32_t*)c.scratch.get("seqc_tmp", seqc_tmp_words(n_ids) * 4);
+    uint64_t* big = (uint64_t*)c.scratch.get("seq_items", (size_t)n_seq * 8);
+    const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s);
+    if (maxdeg >= seqc_threshold()) {
+      HIP_CHECK(hipMemcpyAsync(c.h_pinned + 2, first, 4, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      const uint32_t base = c.h_pinned[2], n_big = n_seq - base;
+      uint64_t* big_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_big * 8);
+      uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_big) * 4);
+      uint64_t* sorted = radix_sort_u64(big, big_b, big, n_big, 0, bits_for(maxdeg), tmp, s);
+      launch_unpack_seq(sorted, 0, n_big, d_seq, d_rank, s, nsd, selfc, mode, base);
+    }
+    if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
+    return n_seq;
+  }
   if (d_rank) launch_fill(d_rank, INV, n_ids, s);
-  if (n_seq == 0) return 0;
   int passes = (bits_for(maxdeg) + 7) / 8;
   uint64_t* items = (uint64_t*)c.scratch.get("seq_items", (size_t)n_ids * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_ids * 8);
   uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
-  if (knobs().seq_compact) {  // 0: sort all n_ids (zeros first)
+  if (knobs().seq_sort) {  // 1: radix sort of the ids with degree > 0; 0: of all n_ids (zeros first)
     uint32_t* ptmp = (uint32_t*)c.scratch.get("seq_pack_tmp", pack_nz_tmp_words(n_ids) * 4);
     launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
     uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);

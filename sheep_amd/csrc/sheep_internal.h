@@ -40,7 +40,8 @@ struct Knobs {
   int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
                          //   after it (1), in line (0), fused into the degree scatter (3,
                          //   graph2tree_dev; taken anyway from 2^31 records)
-  int seq_compact = 1;   // SHEEP_SEQ_COMPACT: sort only the ids with degree > 0
+  int seq_sort = 1;      // SHEEP_SEQ_SORT: the sequence by a counting sort over degree classes (2),
+                         //   a radix sort of the ids with degree > 0 (1) or of all ids (0)
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
   int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)
   int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
@@ -134,7 +135,15 @@ void launch_pack_nonzero(const uint32_t* deg, uint32_t n, uint64_t* items, uint3
                          hipStream_t s);
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
                        uint32_t* rank, hipStream_t s, uint32_t* nsd = nullptr,
-                       const uint32_t* selfc = nullptr, int file_mode = 0);
+                       const uint32_t* selfc = nullptr, int file_mode = 0,
+                       uint32_t base = 0 /* first sequence position written */);
+// Counting-sort sequence (k_seqc_*): seq/rank/nsd of every id of degree 1 .. seqc_threshold()-1,
+// rank INVALID for degree 0; the ids of higher degree go to big as (deg << 32 | id) in id order,
+// to be sorted and unpacked from the position the returned device word (u64) holds.
+size_t seqc_tmp_words(uint32_t n);
+uint32_t seqc_threshold();
+uint32_t* launch_seqc_place(const uint32_t* deg, uint32_t n, uint32_t* seq, uint32_t* rank,
+                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s);
 // nsd[rank[v]] -= w * selfc[v] (w = 2 in FILE mode): the self-loop part of launch_unpack_seq's nsd.
 void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t* rank,
                           int file_mode, uint32_t* nsd, hipStream_t s);

@@ -1343,13 +1343,13 @@ __global__ void k_pack_deg(const uint32_t* __restrict__ deg, uint32_t n, uint64_
 __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros, uint32_t n_seq,
                              uint32_t* __restrict__ seq, uint32_t* __restrict__ rank,
                              uint32_t* __restrict__ nsd, const uint32_t* __restrict__ selfc,
-                             uint32_t w) {
+                             uint32_t w, uint32_t base) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_seq; i += gridDim.x * blockDim.x) {
     const uint64_t it = items[zeros + i];
     uint32_t v = (uint32_t)it;
-    seq[i] = v;
-    if (rank) rank[v] = i;
-    if (nsd) nsd[i] = (uint32_t)(it >> 32);
+    seq[base + i] = v;
+    if (rank) rank[v] = base + i;
+    if (nsd) nsd[base + i] = (uint32_t)(it >> 32);
   }
 }
 
@@ -1429,10 +1429,10 @@ void launch_pack_deg(const uint32_t* deg, uint32_t n, uint64_t* items, hipStream
 
 void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, uint32_t* seq,
                        uint32_t* rank, hipStream_t s, uint32_t* nsd, const uint32_t* selfc,
-                       int file_mode) {
+                       int file_mode, uint32_t base) {
   if (n_seq)
     hipLaunchKernelGGL(k_unpack_seq, dim3(grid_for(n_seq)), dim3(BLOCK), 0, s, items, zeros, n_seq,
-                       seq, rank, nsd, selfc, file_mode ? 2u : 1u);
+                       seq, rank, nsd, selfc, file_mode ? 2u : 1u, base);
 }
 
 void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t* rank,
@@ -1441,6 +1441,123 @@ void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t*
     hipLaunchKernelGGL(k_nsd_selfloops, dim3(grid_for(n_ids)), dim3(BLOCK), 0, s, selfc, n_ids, rank,
                        file_mode ? 2u : 1u, nsd);
 }
+
+// ---------------------------------------------------------------------------------------
+// Degree sequence by counting (sequence.h:55-61: the ids with deg > 0 by degree, ties in id
+// order).  Degrees 1 .. SQ_T-1 are classes of a counting sort straight from deg[] — no items,
+// no radix passes; the few ids of degree >= SQ_T share the last class and are radix-sorted
+// among themselves behind the others.  A chunk is 16 waves x SQ_IT rounds of 64 consecutive
+// ids, wave w owning ids [w 64 SQ_IT, (w + 1) 64 SQ_IT) of it: the per-wave stable rank of
+// k_rsort_scatter then gives id order inside each class.
+//   k_seqc_count   per-chunk class counts (tile-major), then tm_offsets: each chunk's first
+//                  position of every class;
+//   k_seqc_place   seq[pos] = id, rank[id] = pos, nsd[pos] = deg for the counted classes,
+//                  rank[id] = INVALID for degree 0, (deg << 32 | id) for the last class.
+// ---------------------------------------------------------------------------------------
+static constexpr int SQ_DB = 10;
+static constexpr uint32_t SQ_T = 1u << SQ_DB;  // == the block size: one class per thread
+static constexpr int SQ_IT = 16;
+static constexpr uint32_t SQ_CHUNK = 1024u * SQ_IT;
+
+__device__ __forceinline__ uint32_t seqc_class(uint32_t d) { return (min(d, SQ_T) - 1) & (SQ_T - 1); }
+
+__global__ void __launch_bounds__(1024)
+k_seqc_count(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t hist[SQ_T];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  hist[t] = 0;
+  block_sync();
+  const uint64_t base = (uint64_t)blockIdx.x * SQ_CHUNK + (uint64_t)w * (64 * SQ_IT) + lane;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t d[SQ_IT];
+#pragma unroll
+  for (int k = 0; k < SQ_IT; ++k) {
+    const uint64_t id = base + (uint64_t)k * 64;
+    d[k] = id < n ? deg[id] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < SQ_IT; ++k) {
+    const uint32_t c = seqc_class(d[k]);
+    const uint64_t match = digit_match<SQ_DB>(c, d[k] != 0);  // one LDS add per class and round
+    if (d[k] && (match & lt) == 0) atomicAdd(&hist[c], (uint32_t)__popcll(match));
+  }
+  block_sync();
+  counts[(uint64_t)blockIdx.x * SQ_T + t] = hist[t];
+}
+
+__global__ void __launch_bounds__(1024)
+k_seqc_place(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __restrict__ offsets,
+             const unsigned long long* __restrict__ cstart, uint32_t* __restrict__ seq,
+             uint32_t* __restrict__ rank, uint32_t* __restrict__ nsd, uint64_t* __restrict__ big) {
+  __shared__ uint32_t whist[16][SQ_T];  // per-wave class counts, then per-wave offsets
+  __shared__ uint32_t goff[SQ_T];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  goff[t] = offsets[(uint64_t)blockIdx.x * SQ_T + t];
+  for (uint32_t i = lane; i < SQ_T; i += 64) whist[w][i] = 0;
+  const uint32_t big0 = (uint32_t)cstart[SQ_T - 1];
+  block_sync();
+  const uint64_t base = (uint64_t)blockIdx.x * SQ_CHUNK + (uint64_t)w * (64 * SQ_IT) + lane;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t d[SQ_IT], rk[SQ_IT];
+#pragma unroll
+  for (int k = 0; k < SQ_IT; ++k) {
+    const uint64_t id = base + (uint64_t)k * 64;
+    d[k] = id < n ? deg[id] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < SQ_IT; ++k) {  // rounds in id order, lanes in id order within a round
+    const uint32_t c = seqc_class(d[k]);
+    const uint64_t match = digit_match<SQ_DB>(c, d[k] != 0);
+    const uint32_t before = (uint32_t)__popcll(match & lt);
+    const uint32_t prev = whist[w][c];
+    rk[k] = prev + before;
+    if (d[k] && before == 0) whist[w][c] = prev + (uint32_t)__popcll(match);
+  }
+  block_sync();
+  {  // thread t = class t: the waves' exclusive offsets inside the chunk's run of the class
+    uint32_t run = goff[t];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { const uint32_t v = whist[i][t]; whist[i][t] = run; run += v; }
+  }
+  block_sync();
+#pragma unroll
+  for (int k = 0; k < SQ_IT; ++k) {
+    const uint64_t id = base + (uint64_t)k * 64;
+    if (id >= n) continue;
+    if (d[k] == 0) {
+      if (rank) rank[id] = INV;
+    } else if (d[k] < SQ_T) {
+      const uint32_t pos = whist[w][d[k] - 1] + rk[k];
+      seq[pos] = (uint32_t)id;
+      if (rank) rank[id] = pos;
+      if (nsd) nsd[pos] = d[k];
+    } else {
+      big[whist[w][SQ_T - 1] + rk[k] - big0] = ((uint64_t)d[k] << 32) | id;
+    }
+  }
+}
+
+size_t seqc_tmp_words(uint32_t n) {
+  const uint64_t nc = ((uint64_t)n + SQ_CHUNK - 1) / SQ_CHUNK;
+  return SQ_T * nc + SQ_T * ((nc + TM_G - 1) / TM_G) + 2 * (SQ_T + 1) + 2;
+}
+
+uint32_t* launch_seqc_place(const uint32_t* deg, uint32_t n, uint32_t* seq, uint32_t* rank,
+                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s) {
+  const uint32_t nc = (uint32_t)(((uint64_t)n + SQ_CHUNK - 1) / SQ_CHUNK);
+  uint32_t* counts = tmp;
+  uint32_t* gsum = counts + (size_t)SQ_T * nc;
+  unsigned long long* cstart = (unsigned long long*)(((uintptr_t)(gsum + (size_t)SQ_T *
+                                ((nc + TM_G - 1) / TM_G)) + 7) & ~(uintptr_t)7);
+  if (n == 0) return nullptr;
+  hipLaunchKernelGGL(k_seqc_count, dim3(nc), dim3(1024), 0, s, deg, n, counts);
+  tm_offsets(counts, counts, nc, SQ_T, SQ_T, gsum, cstart, s);
+  hipLaunchKernelGGL(k_seqc_place, dim3(nc), dim3(1024), 0, s, deg, n, (const uint32_t*)counts,
+                     (const unsigned long long*)cstart, seq, rank, nsd, big);
+  return (uint32_t*)(cstart + (SQ_T - 1));  // the first position of the last class (u64)
+}
+
+uint32_t seqc_threshold() { return SQ_T; }
 
 // ---------------------------------------------------------------------------------------
 // rank[seq[i]] = i (JTree::insert(X, id), jtree.h:165-168).  A repeated id trips the

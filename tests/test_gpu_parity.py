@@ -80,7 +80,52 @@ def test_rmat_generator_and_tree(oracle, api, gpu, scale, seed):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
+def _degrees(case, rng):
+    if case == "heavy":     # zipf tail: every counting class, hundreds of ids above 1024
+        d = np.minimum(rng.zipf(1.6, 300001), 1 << 31).astype(np.uint32)
+        d[rng.random(d.size) < 0.3] = 0
+    elif case == "small":   # no id reaches the radix-sorted class
+        d = rng.integers(0, 50, 5000, dtype=np.uint32)
+    elif case == "ones":    # one class, off the 16384-id chunk
+        d = np.ones(40000, np.uint32)
+        d[rng.integers(0, d.size, 100)] = 0
+    elif case == "zeros":
+        d = np.zeros(20000, np.uint32)
+    elif case == "full":    # degrees over the whole u32 range, and the class edges 1023/1024
+        d = rng.integers(0, 1 << 32, 70000, dtype=np.uint64).astype(np.uint32)
+        m = rng.random(d.size) < 0.5
+        d[m] = rng.integers(1020, 1028, int(m.sum()), dtype=np.uint32)
+        d[::7] = 1023
+        d[::11] = 1024
+        d[-1] = 0xFFFFFFFF
+    else:                   # one id
+        d = np.array([5], np.uint32)
+    return d
+
+
+@pytest.mark.parametrize("seq_sort", [2, 1, 0])
+@pytest.mark.parametrize("case", ["heavy", "small", "ones", "zeros", "full", "one"])
+def test_sequence_from_degrees(oracle, gpu, options, seq_sort, case):
+    """sheep_sequence_dev on crafted degree vectors (sequence.h:55-61: degree > 0, by degree,
+    ties in id order) under each sort: the counting sort's classes below 1024 and the radix-
+    sorted ids above, ties, zero degrees, sizes off its 16384-id chunk, degrees up to 2^32-1."""
+    import torch
+    from sheep_amd import device
+
+    options(seq_sort=seq_sort)
+    d = _degrees(case, np.random.default_rng(len(case)))
+    seq, rank, n = device.sequence(torch.from_numpy(d.view(np.int32)).cuda().view(torch.uint32))
+    torch.cuda.synchronize()
+    want = oracle.sequence(d)
+    assert n == want.size
+    assert np.array_equal(seq[:n].cpu().numpy().view(np.uint32), want)
+    rk = np.full(d.size, 0xFFFFFFFF, np.uint32)
+    rk[want] = np.arange(want.size, dtype=np.uint32)
+    assert np.array_equal(rank[:d.size].cpu().numpy().view(np.uint32), rk)
+
+
 @pytest.mark.parametrize("scale,seed,mode,env", [
+    (18, 33, 0, {"seq_sort": 1}),           # the radix-sorted sequence (the counting sort's A/B)
     (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
     (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
     (16, 23, 0, {"edge_part": 1}),  # the partitioned gathers at a small size
