@@ -39,6 +39,7 @@ struct KnobDef {
 static const KnobDef kKnobs[] = {
     {"degree", &Knobs::degree},           {"edge_part", &Knobs::edge_part},
     {"part_overlap", &Knobs::part_overlap}, {"seq_sort", &Knobs::seq_sort},
+    {"part_ysort", &Knobs::part_ysort},
     {"kb_buckets", &Knobs::kb_buckets},
     {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
     {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},

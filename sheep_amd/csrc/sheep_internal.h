@@ -40,7 +40,9 @@ struct Knobs {
   int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
                          //   after it (1), in line (0), fused into the degree scatter (3,
                          //   graph2tree_dev; taken anyway from 2^31 records)
-  int seq_sort = 1;      // SHEEP_SEQ_SORT: the sequence by a counting sort over degree classes (2),
+  int part_ysort = 1;    // SHEEP_PART_YSORT: the second partition pass orders each tile by y
+                         //   before its rank gathers (cache-line sharing)
+  int seq_sort = 2;      // SHEEP_SEQ_SORT: the sequence by a counting sort over degree classes (2),
                          //   a radix sort of the ids with degree > 0 (1) or of all ids (0)
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
   int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)

@@ -1945,7 +1945,7 @@ template <int MODE, int NT, int IT, uint32_t ND>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
-       const uint32_t* __restrict__ rank, uint32_t n_rank) {
+       const uint32_t* __restrict__ rank, uint32_t n_rank, int ysh) {
   static_assert(ND % NT == 0 || NT % ND == 0, "digits per thread");
   constexpr int R = ND > (uint32_t)NT ? (int)ND / NT : 1;  // digits per thread in the scan
   constexpr int PT_ITEMS = IT;
@@ -1965,6 +1965,40 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   for (int k = 0; k < PT_ITEMS; ++k) {
     uint32_t j = (uint32_t)k * NT + t;
     rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+  }
+  if (MODE == 1 && ysh >= 0) {
+    // The tile in y order first, by 256 sub-ranges of its y digit (counting sort in LDS): the
+    // 64 gathers of a wave then fall in a few 256-id sub-ranges and share cache lines, where
+    // in stream order each is an L2 request of its own (the pass is bound by those requests).
+    static_assert(MODE != 1 || ND == 256, "sub-ranges use the x-digit arrays");
+    block_sync();
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k)
+      if ((uint32_t)k * NT + t < tile_n) li[k] = atomicAdd(&hist[(uint32_t)(rec[k] >> (32 + ysh)) & 255u], 1u);
+    block_sync();
+    if (t < 256) {
+      const uint32_t c = hist[t], incl = wave_incl_scan(c);
+      if (lane == 63) wsum[w] = incl;
+      tstart[t] = incl - c;
+    }
+    block_sync();
+    if (t < 256) {
+      uint32_t add = 0;
+      for (int i = 0; i < w; ++i) add += wsum[i];
+      tstart[t] += add;
+      hist[t] = 0;
+    }
+    block_sync();
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k)
+      if ((uint32_t)k * NT + t < tile_n)
+        stage[tstart[(uint32_t)(rec[k] >> (32 + ysh)) & 255u] + li[k]] = rec[k];
+    block_sync();
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      rec[k] = j < tile_n ? stage[j] : 0ull;
+    }
   }
   if (MODE == 1) {  // (x, y) -> (x, ry)
     uint32_t ry[PT_ITEMS];
@@ -2049,19 +2083,20 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
   hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt), dim3(PT0_THREADS),
                      0, s, (const uint64_t*)uv, m, mid, cursor, xhist, sh, shx,
-                     (const uint32_t*)nullptr, n_rank);
+                     (const uint32_t*)nullptr, n_rank, -1);
 }
 
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s) {
   if (m == 0) return;
   const int shx = part_shift(n_rank, PD_X);
+  const int ysh = knobs().part_ysort ? std::max(part_shift(n_rank, PD_Y) - 8, 0) : -1;
   uint32_t* xhist = ws + PW_X;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_CUR);
-  uint64_t nt = (m + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
   hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor);
+  uint64_t nt = (m + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
   hipLaunchKernelGGL((k_part<1, PT1_THREADS, PT1_ITEMS, PD_X>), dim3((unsigned)nt), dim3(PT1_THREADS),
-                     0, s, mid, m, pre, cursor, xhist, shx, shx, rank, n_rank);
+                     0, s, mid, m, pre, cursor, xhist, shx, shx, rank, n_rank, ysh);
 }
 
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,

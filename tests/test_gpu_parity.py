@@ -126,6 +126,8 @@ def test_sequence_from_degrees(oracle, gpu, options, seq_sort, case):
 
 @pytest.mark.parametrize("scale,seed,mode,env", [
     (18, 33, 0, {"seq_sort": 1}),           # the radix-sorted sequence (the counting sort's A/B)
+    (18, 34, 1, {"seq_sort": 1}),           # the same, FILE degrees
+    (18, 35, 0, {"part_ysort": 0}),         # second partition pass gathering in stream order
     (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
     (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
     (16, 23, 0, {"edge_part": 1}),  # the partitioned gathers at a small size
