@@ -360,7 +360,9 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   if (knobs().seq_sort == 2) {  // counting sort by degree; radix only for degrees >= 1024
     uint32_t* qtmp = (uint32_t*)c.scratch.get("seqc_tmp", seqc_tmp_words(n_ids) * 4);
     uint64_t* big = (uint64_t*)c.scratch.get("seq_items", (size_t)n_seq * 8);
-    const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s);
+    const uint32_t* sc = nsd ? selfc : nullptr;  // the self-loop records off nsd in place
+    const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s, sc,
+                                              mode);
     if (maxdeg >= seqc_threshold()) {
       HIP_CHECK(hipMemcpyAsync(c.h_pinned + 2, first, 4, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
@@ -368,9 +370,8 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
       uint64_t* big_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_big * 8);
       uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_big) * 4);
       uint64_t* sorted = radix_sort_u64(big, big_b, big, n_big, 0, bits_for(maxdeg), tmp, s);
-      launch_unpack_seq(sorted, 0, n_big, d_seq, d_rank, s, nsd, selfc, mode, base);
+      launch_unpack_seq(sorted, 0, n_big, d_seq, d_rank, s, nsd, sc, mode, base);
     }
-    if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
     return n_seq;
   }
   if (d_rank) launch_fill(d_rank, INV, n_ids, s);
@@ -382,13 +383,13 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
     uint32_t* ptmp = (uint32_t*)c.scratch.get("seq_pack_tmp", pack_nz_tmp_words(n_ids) * 4);
     launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
     uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);
-    launch_unpack_seq(sorted, 0, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
+    launch_unpack_seq(sorted, 0, n_seq, d_seq, d_rank, s, nsd, nullptr, mode);
     if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
     return n_seq;
   }
   launch_pack_deg(d_deg, n_ids, items, s);
   uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
-  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, selfc, mode);
+  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, nullptr, mode);
   if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
   return n_seq;
 }

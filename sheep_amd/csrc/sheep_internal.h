@@ -144,8 +144,10 @@ void launch_unpack_seq(const uint64_t* items, uint32_t zeros, uint32_t n_seq, ui
 // to be sorted and unpacked from the position the returned device word (u64) holds.
 size_t seqc_tmp_words(uint32_t n);
 uint32_t seqc_threshold();
+// selfc (nullable): nsd = deg - w * selfc (w = 2 in FILE mode), as launch_nsd_selfloops.
 uint32_t* launch_seqc_place(const uint32_t* deg, uint32_t n, uint32_t* seq, uint32_t* rank,
-                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s);
+                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s,
+                            const uint32_t* selfc, int file_mode);
 // nsd[rank[v]] -= w * selfc[v] (w = 2 in FILE mode): the self-loop part of launch_unpack_seq's nsd.
 void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t* rank,
                           int file_mode, uint32_t* nsd, hipStream_t s);

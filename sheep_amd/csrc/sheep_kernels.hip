@@ -333,9 +333,10 @@ __device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, ui
   }
 }
 // Tile-major count matrices and their scan (defined with the hi bins below).
-static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
-                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s);
 static constexpr uint32_t TM_G = 256;  // tiles per group
+static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
+                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s,
+                       uint32_t G = TM_G);
 static constexpr int DEGB_CHUNK = 32768;  // edges per chunk (<= 65536 endpoints -> 128 KB LDS)
 static constexpr uint32_t DEGB_NB = 1024;
 static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgroup
@@ -1124,8 +1125,8 @@ k_rsort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uin
 
 __global__ void __launch_bounds__(1024)
 k_tm_colsum(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t NC,
-            uint32_t* __restrict__ gsum) {
-  const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
+            uint32_t* __restrict__ gsum, uint32_t G) {
+  const uint32_t d = threadIdx.x, t0 = blockIdx.x * G, t1 = min(t0 + G, ntiles);
   if (d >= NC) return;
   uint32_t sum = 0;
   for (uint32_t t = t0; t < t1; t += 8) {
@@ -1171,8 +1172,8 @@ k_tm_scan_groups(uint32_t* __restrict__ gsum, uint32_t ngroups, uint32_t NC, uin
 __global__ void __launch_bounds__(1024)
 k_tm_rows(const uint32_t* in, uint32_t* out, uint32_t ntiles, uint32_t NC,
           const uint32_t* __restrict__ gsum, const unsigned long long* __restrict__ bin_start,
-          uint32_t nb) {
-  const uint32_t d = threadIdx.x, t0 = blockIdx.x * TM_G, t1 = min(t0 + TM_G, ntiles);
+          uint32_t nb, uint32_t G) {
+  const uint32_t d = threadIdx.x, t0 = blockIdx.x * G, t1 = min(t0 + G, ntiles);
   if (d >= NC) return;
   uint32_t run = (d < nb ? (uint32_t)bin_start[d] : 0u) + gsum[(uint64_t)blockIdx.x * NC + d];
   for (uint32_t t = t0; t < t1; t += 8) {
@@ -1187,16 +1188,18 @@ k_tm_rows(const uint32_t* in, uint32_t* out, uint32_t ntiles, uint32_t NC,
   }
 }
 
-// Tile-major exclusive offsets of an ntiles x NC count matrix (gsum: NC * ceil(ntiles / TM_G)
-// words of scratch); bin_start: nb + 1 u64 (column starts, then the total).
+// Tile-major exclusive offsets of an ntiles x NC count matrix (gsum: NC * ceil(ntiles / G)
+// words of scratch); bin_start: nb + 1 u64 (column starts, then the total).  G: tiles per
+// group (the column and row passes run one block per group).
 static void tm_offsets(const uint32_t* counts, uint32_t* offsets, uint32_t ntiles, uint32_t NC,
-                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s) {
-  const uint32_t ng = (ntiles + TM_G - 1) / TM_G;
+                       uint32_t nb, uint32_t* gsum, unsigned long long* bin_start, hipStream_t s,
+                       uint32_t G) {
+  const uint32_t ng = (ntiles + G - 1) / G;
   const unsigned th = NC <= 512 ? 512 : 1024;
-  hipLaunchKernelGGL(k_tm_colsum, dim3(ng), dim3(th), 0, s, counts, ntiles, NC, gsum);
+  hipLaunchKernelGGL(k_tm_colsum, dim3(ng), dim3(th), 0, s, counts, ntiles, NC, gsum, G);
   hipLaunchKernelGGL(k_tm_scan_groups, dim3(1), dim3(th), 0, s, gsum, ng, NC, nb, bin_start);
   hipLaunchKernelGGL(k_tm_rows, dim3(ng), dim3(th), 0, s, counts, offsets, ntiles, NC,
-                     (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb);
+                     (const uint32_t*)gsum, (const unsigned long long*)bin_start, nb, G);
 }
 
 // The hi-bin scatter without stability (the order inside a bin is free: the kb loop and pst
@@ -1337,9 +1340,9 @@ __global__ void k_pack_deg(const uint32_t* __restrict__ deg, uint32_t n, uint64_
     items[i] = ((uint64_t)deg[i] << 32) | i;
 }
 
-// nsd (nullable): nsd[i] = degree of seq[i] in rank order (the sorted item's key); the
-// self-loop records are taken off afterwards by k_nsd_selfloops (rare: a sparse pass instead
-// of a gather per rank).
+// nsd (nullable): nsd[i] = degree of seq[i] in rank order (the sorted item's key), less
+// w * selfc[seq[i]] when selfc is given; otherwise k_nsd_selfloops takes the self-loop records
+// off afterwards (a sparse pass instead of a gather per rank).
 __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros, uint32_t n_seq,
                              uint32_t* __restrict__ seq, uint32_t* __restrict__ rank,
                              uint32_t* __restrict__ nsd, const uint32_t* __restrict__ selfc,
@@ -1349,7 +1352,7 @@ __global__ void k_unpack_seq(const uint64_t* __restrict__ items, uint32_t zeros,
     uint32_t v = (uint32_t)it;
     seq[base + i] = v;
     if (rank) rank[v] = base + i;
-    if (nsd) nsd[base + i] = (uint32_t)(it >> 32);
+    if (nsd) nsd[base + i] = (uint32_t)(it >> 32) - (selfc ? w * selfc[v] : 0u);
   }
 }
 
@@ -1458,6 +1461,7 @@ static constexpr int SQ_DB = 10;
 static constexpr uint32_t SQ_T = 1u << SQ_DB;  // == the block size: one class per thread
 static constexpr int SQ_IT = 16;
 static constexpr uint32_t SQ_CHUNK = 1024u * SQ_IT;
+static constexpr uint32_t SQ_G = 16;  // chunks per group of tm_offsets' column and row passes
 
 __device__ __forceinline__ uint32_t seqc_class(uint32_t d) { return (min(d, SQ_T) - 1) & (SQ_T - 1); }
 
@@ -1488,7 +1492,8 @@ k_seqc_count(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* __restrict_
 __global__ void __launch_bounds__(1024)
 k_seqc_place(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __restrict__ offsets,
              const unsigned long long* __restrict__ cstart, uint32_t* __restrict__ seq,
-             uint32_t* __restrict__ rank, uint32_t* __restrict__ nsd, uint64_t* __restrict__ big) {
+             uint32_t* __restrict__ rank, uint32_t* __restrict__ nsd, uint64_t* __restrict__ big,
+             const uint32_t* __restrict__ selfc, uint32_t sw) {
   __shared__ uint32_t whist[16][SQ_T];  // per-wave class counts, then per-wave offsets
   __shared__ uint32_t goff[SQ_T];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1530,7 +1535,7 @@ k_seqc_place(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __res
       const uint32_t pos = whist[w][d[k] - 1] + rk[k];
       seq[pos] = (uint32_t)id;
       if (rank) rank[id] = pos;
-      if (nsd) nsd[pos] = d[k];
+      if (nsd) nsd[pos] = d[k] - (selfc ? sw * selfc[id] : 0u);
     } else {
       big[whist[w][SQ_T - 1] + rk[k] - big0] = ((uint64_t)d[k] << 32) | id;
     }
@@ -1539,21 +1544,23 @@ k_seqc_place(const uint32_t* __restrict__ deg, uint32_t n, const uint32_t* __res
 
 size_t seqc_tmp_words(uint32_t n) {
   const uint64_t nc = ((uint64_t)n + SQ_CHUNK - 1) / SQ_CHUNK;
-  return SQ_T * nc + SQ_T * ((nc + TM_G - 1) / TM_G) + 2 * (SQ_T + 1) + 2;
+  return SQ_T * nc + SQ_T * ((nc + SQ_G - 1) / SQ_G) + 2 * (SQ_T + 1) + 2;
 }
 
 uint32_t* launch_seqc_place(const uint32_t* deg, uint32_t n, uint32_t* seq, uint32_t* rank,
-                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s) {
+                            uint32_t* nsd, uint64_t* big, uint32_t* tmp, hipStream_t s,
+                            const uint32_t* selfc, int file_mode) {
   const uint32_t nc = (uint32_t)(((uint64_t)n + SQ_CHUNK - 1) / SQ_CHUNK);
   uint32_t* counts = tmp;
   uint32_t* gsum = counts + (size_t)SQ_T * nc;
   unsigned long long* cstart = (unsigned long long*)(((uintptr_t)(gsum + (size_t)SQ_T *
-                                ((nc + TM_G - 1) / TM_G)) + 7) & ~(uintptr_t)7);
+                                ((nc + SQ_G - 1) / SQ_G)) + 7) & ~(uintptr_t)7);
   if (n == 0) return nullptr;
   hipLaunchKernelGGL(k_seqc_count, dim3(nc), dim3(1024), 0, s, deg, n, counts);
-  tm_offsets(counts, counts, nc, SQ_T, SQ_T, gsum, cstart, s);
+  tm_offsets(counts, counts, nc, SQ_T, SQ_T, gsum, cstart, s, SQ_G);
   hipLaunchKernelGGL(k_seqc_place, dim3(nc), dim3(1024), 0, s, deg, n, (const uint32_t*)counts,
-                     (const unsigned long long*)cstart, seq, rank, nsd, big);
+                     (const unsigned long long*)cstart, seq, rank, nsd, big, selfc,
+                     file_mode ? 2u : 1u);
   return (uint32_t*)(cstart + (SQ_T - 1));  // the first position of the last class (u64)
 }
 
