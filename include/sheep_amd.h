@@ -81,9 +81,9 @@ int sheep_abi_version(void);
 /* Tuning options (sheep_amd/csrc/sheep_internal.h, struct Knobs): they move work between
  * kernels and never change a result.  Their defaults come from SHEEP_<NAME> environment
  * variables, read ONCE when the library first initialises a device; afterwards only these
- * calls change them (process-wide).  Names: degree, edge_part, part_overlap, seq_sort,
- * kb_buckets, kb_rankb, kb_pipe, kb_refresh, kb_gbits, kb_defer, degb_plain, degb_hist,
- * tree_stats, bin_direct, bin_slack, kb_pick, kb_drop, kb_gsum, eval_pass, ls_split, ls_seq.
+ * calls change them (process-wide).  Names: degree, edge_part, part_overlap, kb_buckets,
+ * kb_rankb, kb_pipe, tree_stats, bin_direct, bin_slack, kb_gsum, eval_pass, ls_split, ls_seq
+ * (and the lab option kb_merge).
  * -EINVAL for an unknown name. */
 int sheep_set_option(const char* name, long long value);
 int sheep_get_option(const char* name, long long* value);

@@ -208,10 +208,12 @@ def mpi_sequence(uv, n_ids=0, mode=DEGREE_LLAMA):
     n = ctypes.c_uint32(0)
     rc = capi.lib().sheep_mpi_sequence(_ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
                                        ctypes.byref(n))
-    if rc == -errno.ERANGE and n.value > cap:
-        # this rank's ids do not span the sequence: every rank got -ERANGE with the global
-        # length (the smallest buffer of all ranks decides), so all retry together
-        cap = n.value
+    if rc == -errno.ERANGE and n.value > 0:
+        # some rank's ids do not span the sequence: EVERY rank got -ERANGE with the global
+        # length (the smallest buffer of all ranks decides), so every rank retries, including
+        # those whose own buffer was large enough (else they would leave the others waiting in
+        # the retry's collectives)
+        cap = max(cap, n.value)
         seq = np.zeros(cap, np.uint32)
         rc = capi.lib().sheep_mpi_sequence(_ptr(uv), uv.shape[0], n_ids, mode, _ptr(seq), cap,
                                            ctypes.byref(n))

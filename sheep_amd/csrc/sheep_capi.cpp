@@ -38,18 +38,13 @@ struct KnobDef {
 };
 static const KnobDef kKnobs[] = {
     {"degree", &Knobs::degree},           {"edge_part", &Knobs::edge_part},
-    {"part_overlap", &Knobs::part_overlap}, {"seq_sort", &Knobs::seq_sort},
-    {"part_ysort", &Knobs::part_ysort},
-    {"kb_buckets", &Knobs::kb_buckets},
-    {"kb_rankb", &Knobs::kb_rankb},       {"kb_pipe", &Knobs::kb_pipe},
-    {"kb_refresh", &Knobs::kb_refresh},   {"kb_gbits", &Knobs::kb_gbits},
-    {"kb_defer", &Knobs::kb_defer},
-    {"degb_plain", &Knobs::degb_plain},   {"degb_hist", &Knobs::degb_hist16},
-    {"tree_stats", &Knobs::tree_stats},
+    {"part_overlap", &Knobs::part_overlap},
+    {"kb_buckets", &Knobs::kb_buckets},   {"kb_rankb", &Knobs::kb_rankb},
+    {"kb_pipe", &Knobs::kb_pipe},         {"tree_stats", &Knobs::tree_stats},
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
-    {"kb_pick", &Knobs::kb_pick},         {"kb_drop", &Knobs::kb_drop},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
+    {"kb_merge", &Knobs::kb_merge},
 };
 
 static Knobs g_knobs;
@@ -88,6 +83,20 @@ struct ApiError : std::runtime_error {
       throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));                         \
   } while (0)
 
+// SHEEP_SCRATCH_LOG=1: every allocation's name, address and size on stderr (diagnostics: where
+// the big buffers land, DESIGN.md §9 "run-to-run spread").
+static bool scratch_log() {
+  static const bool on = getenv("SHEEP_SCRATCH_LOG") && atoi(getenv("SHEEP_SCRATCH_LOG")) != 0;
+  return on;
+}
+
+static void scratch_alloc(void** p, size_t bytes, const char* name) {
+  HIP_CHECK(hipMalloc(p, bytes));
+  if (scratch_log())
+    fprintf(stderr, "scratch %s %p %zu (2MB-aligned %d)\n", name, *p, bytes,
+            (int)(((uintptr_t)*p & ((2u << 20) - 1)) == 0));
+}
+
 void* Scratch::get(const char* name, size_t bytes) {
   if (bytes == 0) bytes = 4;
   for (auto& s : slots) {
@@ -96,13 +105,13 @@ void* Scratch::get(const char* name, size_t bytes) {
       HIP_CHECK(hipFree(s.second.p));
       s.second.p = nullptr;
       s.second.bytes = 0;
-      HIP_CHECK(hipMalloc(&s.second.p, bytes));
+      scratch_alloc(&s.second.p, bytes, name);
       s.second.bytes = bytes;
       return s.second.p;
     }
   }
   Slot sl;
-  HIP_CHECK(hipMalloc(&sl.p, bytes));
+  scratch_alloc(&sl.p, bytes, name);
   sl.bytes = bytes;
   slots.emplace_back(name, sl);
   return sl.p;
@@ -260,6 +269,36 @@ static void check_err(Ctx& c, hipStream_t s) {
   }
 }
 
+// check_err for a group: every rank's error word and walk guard, MAX-reduced over the ranks, so
+// that a fault on one rank (whose corrupt forest the parent sum hands to all) fails the call on
+// every rank, after the same collectives.  Synchronises s.
+static void check_err_group(Ctx& c, Comm& comm, hipStream_t s) {
+  uint32_t* fw = fault_word();
+  HIP_CHECK(hipMemcpyAsync(c.h_pinned, c.d_err, 4, hipMemcpyDeviceToHost, s));
+  c.h_pinned[12] = 0;
+  if (fw) HIP_CHECK(hipMemcpyAsync(c.h_pinned + 12, fw, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  int64_t h = ((int64_t)c.h_pinned[12] << 32) | c.h_pinned[0];
+  if (comm.size() > 1) {
+    int64_t* d = (int64_t*)c.scratch.get("mt_err", 8);
+    HIP_CHECK(hipMemcpyAsync(d, &h, 8, hipMemcpyHostToDevice, s));
+    comm.allreduce_max_i64(d, 1, s);
+    HIP_CHECK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+  if (h == 0) return;
+  HIP_CHECK(hipMemsetAsync(c.d_err, 0, 4, s));
+  if (fw) HIP_CHECK(hipMemsetAsync(fw, 0, 4, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  const uint32_t f = (uint32_t)(h >> 32), e = (uint32_t)h;
+  if (f)
+    throw ApiError(-EIO, std::string("device walk guard tripped on a rank (") +
+                             ((f & 1) ? "forest not heap-ordered" : "union-find cycle") +
+                             "): corrupt intermediate data");
+  if (e & ERR_DUP_SEQ) throw ApiError(-EINVAL, "sequence repeats a vertex id");
+  throw ApiError(-ERANGE, "vertex id out of range of the sequence/id space");
+}
+
 // Counters, tile offsets and kept-pair positions of the tree build are u32 (records), and the
 // degree pass's endpoint offsets are u32 (2 per record): reject inputs beyond them.
 static void require_records(uint64_t m, const char* what) {
@@ -331,6 +370,12 @@ struct DegInfo {
   const uint32_t* nsd = nullptr;    // rank-ordered deg - w * selfc (nullable, see sequence_dev)
   bool part_first_done = false;     // the first partition pass was launched on c.side into
                                     // e_items; c.part_ev[1] marks its end
+  bool mid_p6 = false;              // ... and wrote packed 6-byte records (launch_part_first)
+  uint64_t mid_slots = 0;           // ... of which e_items holds this many (0: m)
+  bool mid_caps = false;            // ... into capacity regions (launch_part_first_caps): its
+                                    // overflow word is c.d_err[3]
+  bool ids_checked = false;         // an id >= n_rank fails the call anyway (the degree pass's
+                                    // ERR_RANGE): the partition passes may pack (part_p6_ok)
 };
 
 // Rank gathers in partitioned order (launch_part_gather) for large inputs.
@@ -357,40 +402,20 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
     if (d_rank) launch_fill(d_rank, INV, n_ids, s);
     return 0;
   }
-  if (knobs().seq_sort == 2) {  // counting sort by degree; radix only for degrees >= 1024
-    uint32_t* qtmp = (uint32_t*)c.scratch.get("seqc_tmp", seqc_tmp_words(n_ids) * 4);
-    uint64_t* big = (uint64_t*)c.scratch.get("seq_items", (size_t)n_seq * 8);
-    const uint32_t* sc = nsd ? selfc : nullptr;  // the self-loop records off nsd in place
-    const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s, sc,
-                                              mode);
-    if (maxdeg >= seqc_threshold()) {
-      HIP_CHECK(hipMemcpyAsync(c.h_pinned + 2, first, 4, hipMemcpyDeviceToHost, s));
-      HIP_CHECK(hipStreamSynchronize(s));
-      const uint32_t base = c.h_pinned[2], n_big = n_seq - base;
-      uint64_t* big_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_big * 8);
-      uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_big) * 4);
-      uint64_t* sorted = radix_sort_u64(big, big_b, big, n_big, 0, bits_for(maxdeg), tmp, s);
-      launch_unpack_seq(sorted, 0, n_big, d_seq, d_rank, s, nsd, sc, mode, base);
-    }
-    return n_seq;
+  // counting sort by degree classes; radix sort only for the ids of degree >= 1024
+  uint32_t* qtmp = (uint32_t*)c.scratch.get("seqc_tmp", seqc_tmp_words(n_ids) * 4);
+  uint64_t* big = (uint64_t*)c.scratch.get("seq_items", (size_t)n_seq * 8);
+  const uint32_t* sc = nsd ? selfc : nullptr;  // the self-loop records off nsd in place
+  const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s, sc, mode);
+  if (maxdeg >= seqc_threshold()) {
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 2, first, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    const uint32_t base = c.h_pinned[2], n_big = n_seq - base;
+    uint64_t* big_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_big * 8);
+    uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_big) * 4);
+    uint64_t* sorted = radix_sort_u64(big, big_b, big, n_big, 0, bits_for(maxdeg), tmp, s);
+    launch_unpack_seq(sorted, 0, n_big, d_seq, d_rank, s, nsd, sc, mode, base);
   }
-  if (d_rank) launch_fill(d_rank, INV, n_ids, s);
-  int passes = (bits_for(maxdeg) + 7) / 8;
-  uint64_t* items = (uint64_t*)c.scratch.get("seq_items", (size_t)n_ids * 8);
-  uint64_t* items_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_ids * 8);
-  uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_ids) * 4);
-  if (knobs().seq_sort) {  // 1: radix sort of the ids with degree > 0; 0: of all n_ids (zeros first)
-    uint32_t* ptmp = (uint32_t*)c.scratch.get("seq_pack_tmp", pack_nz_tmp_words(n_ids) * 4);
-    launch_pack_nonzero(d_deg, n_ids, items, ptmp, s);
-    uint64_t* sorted = radix_sort_u64(items, items_b, items, n_seq, 0, 8 * passes, tmp, s);
-    launch_unpack_seq(sorted, 0, n_seq, d_seq, d_rank, s, nsd, nullptr, mode);
-    if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
-    return n_seq;
-  }
-  launch_pack_deg(d_deg, n_ids, items, s);
-  uint64_t* sorted = radix_sort_u64(items, items_b, items, n_ids, 0, 8 * passes, tmp, s);
-  launch_unpack_seq(sorted, zeros, n_seq, d_seq, d_rank, s, nsd, nullptr, mode);
-  if (nsd && selfc && d_rank) launch_nsd_selfloops(selfc, n_ids, d_rank, mode, nsd, s);
   return n_seq;
 }
 
@@ -445,8 +470,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // the giant summary the next map reads (written after each rebase)
   uint32_t* gsum = (uint32_t*)c.scratch.get("kb_gsum", ((size_t)n_seq / 2048 + 2) * 4);
   // the giant's anchor of each map, picked on the device (two slots by bucket parity)
-  uint32_t* anc = knobs().kb_pick ? (uint32_t*)c.scratch.get("kb_anchor", 2 * 4) : nullptr;
-  if (anc) (void)hipMemsetAsync(anc, 0xFF, 2 * 4, s);
+  uint32_t* anc = (uint32_t*)c.scratch.get("kb_anchor", 2 * 4);
+  (void)hipMemsetAsync(anc, 0xFF, 2 * 4, s);
   (void)hipMemsetAsync(counters, 0, 2 * 64, s);
   (void)hipMemsetAsync(bitmaps, 0, 2 * bm_words * 4, s);
   (void)hipMemsetAsync(gx, 0xFF, 2 * 4, s);
@@ -502,22 +527,15 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // j reads slot (j-1) & 1 and writes slot j & 1, at a point where neither stream touches the
   // union-find (map j-1 and apply j-1 complete); an apply uses the slot most recently written
   // on its stream.
-  if (!knobs().kb_gbits) gbits = nullptr;
   // the summary costs a launch per bucket: it pays on large inputs only (RMAT-26 tree 18.5 ->
   // 16.7 ms; RMAT-22 3.25 -> 3.45 ms)
-  if (!gbits || !(knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))) gsum = nullptr;
-  // the map leaves its union-find misses to the apply's refresh kernel (kb_defer)
-  const bool defer = knobs().kb_defer != 0;
+  if (!(knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))) gsum = nullptr;
+  // the map leaves its union-find misses to the apply's refresh kernel
   hipStream_t sa = s;  // the applies and the rebases between them
-  auto rebase = [&](size_t j) {
-    if (anc) {  // the anchor of map j, then the bitmap's rebase on it
-      const uint32_t a = anchor_of(j);
-      launch_kb_pick(uf, a == INV ? 0u : a + 1, anc + ((j - 1) & 1), anc + (j & 1), gbits, n_seq,
-                     gx + ((j - 1) & 1), gx + (j & 1), sa);
-    } else {
-      if (!gbits) return;
-      launch_gb_rebase(gbits, n_seq, uf, anchor_of(j), gx + ((j - 1) & 1), gx + (j & 1), sa);
-    }
+  auto rebase = [&](size_t j) {  // the anchor of map j, then the bitmap's rebase on it
+    const uint32_t a = anchor_of(j);
+    launch_kb_pick(uf, a == INV ? 0u : a + 1, anc + ((j - 1) & 1), anc + (j & 1), gbits, n_seq,
+                   gx + ((j - 1) & 1), gx + (j & 1), sa);
     if (gsum) launch_gb_sum(gbits, n_seq, gsum, sa);
   };
   auto map_k = [&](size_t k, hipStream_t st) {
@@ -532,7 +550,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     launch_kb_map(sorted, seg ? seg->cstart[bk[k].second] : bk[k].second,
                   seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
                   anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
-                  lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, (int)defer,
+                  lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, 1,
                   st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr, k >= 1 ? gsum : nullptr);
     if (tm) tm->span_end(sp, st);
   };
@@ -540,7 +558,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     int p = par(k);
     launch_kb_apply(recs(k) > 0, bk[k].first, bk[k + 1].first, anchor_of(k),
                     uf, label, d_parent, jump, kept[p], linked, bitmaps + p * bm_words,
-                    spqs + p * spq_words, counters + p * 16, defer || (pipe && knobs().kb_refresh), stats,
+                    spqs + p * spq_words, counters + p * 16, true, stats,
                     ws, gbits, gbits ? gx + (slot & 1) : nullptr, st, anc ? anc + (k & 1) : nullptr,
                     anc ? anc + ((k + 1) & 1) : nullptr);
   };
@@ -679,6 +697,19 @@ static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
   }
   std::sort(cuts.begin(), cuts.end());
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  if (knobs().kb_merge > 0) {  // lab: drop a cut while the buckets either side hold few records
+    const uint64_t thr = m_valid * (uint64_t)knobs().kb_merge / 10000;
+    std::vector<uint32_t> kept;
+    uint32_t prev = 0;
+    for (size_t i = 0; i < cuts.size(); ++i) {
+      const uint32_t next = i + 1 < cuts.size() ? cuts[i + 1] : nb - 1;
+      if (bin_start[next] - bin_start[prev] > thr) {
+        kept.push_back(cuts[i]);
+        prev = cuts[i];
+      }
+    }
+    cuts.swap(kept);
+  }
   return cuts;
 }
 
@@ -742,13 +773,18 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     HIP_CHECK(hipMemcpyAsync(c.h_chunks, cds, nch * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(c.bins_ev, s));
   }
+  const bool direct = use_bins && allow_direct && knobs().bin_direct;
+  // the second pass's records packed to 6 bytes: only the direct edge pass reads them
+  const bool pre6 = part && direct && di && di->ids_checked && part_p6_ok(n_rank);
+  uint32_t* pws = part ? (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4) : nullptr;
   if (part) {
-    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
       HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
-      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, di->mid_p6, pre6,
+                         di->mid_slots, di->mid_caps);
     } else {
-      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready);
+      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready,
+                         pre6);
     }
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
@@ -759,7 +795,6 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   const uint32_t* dbins = nullptr;
   uint32_t nbins = 0;
   SegPlan plan;
-  const bool direct = use_bins && allow_direct && knobs().bin_direct;
   uint32_t* ovf = c.d_err + 1;  // a directly binned bin outgrew its capacity
   if (direct) {
     // Each bin gets a capacity region sized by its estimated records (+ slack); the edge pass
@@ -788,16 +823,20 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     uint64_t* binned = (uint64_t*)c.scratch.get(
         "e_binned", std::max<uint64_t>(plan.cstart[nbins - 1], 1) * 8);
     launch_edge_bin(src, part, m, d_rank, n_rank, c.d_err, db, nbins, dseg + 512, dseg + 1024,
-                    binned, ovf, s);
+                    binned, ovf, s, pre6 ? pws : nullptr);
     if (tm) tm->mark("edge_pass");
     // One readback before the kb loop is enqueued (the host then enqueues while the GPU runs
     // the first buckets): a bin that outgrew its estimate holds a hole where its dropped runs
     // were reserved, so the records are grouped again through the scatter.
-    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 8, ovf, 4, hipMemcpyDeviceToHost, s));
+    // (with ovf the first partition pass's overflow word, c.d_err[3]: capacity regions)
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 8, ovf, 12, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (c.h_pinned[8]) {
+    if (c.h_pinned[8] || (di && di->mid_caps && c.h_pinned[10])) {
       DegInfo d2 = *di;
-      d2.part_first_done = false;  // k_part's passes are run again from d_uv
+      d2.part_first_done = false;  // k_part's passes are run again from d_uv (unpacked)
+      d2.mid_p6 = false;
+      d2.mid_caps = false;
+      d2.mid_slots = 0;
       d2.yhist_ready = false;      // the first partition consumed the y-digit counts
       build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, tm, &d2, false);
       return;
@@ -938,6 +977,9 @@ struct Lockstep {
   // per-bucket apply spans ("kb_apply": the one-GPU rehearsal's per-rank apply time); the
   // multi-GPU driver times only the maps
   bool time_apply = true;
+  // the exchange buffers were sized for the whole loop before it started (multi_tree): the
+  // applies never grow them, so nothing inside the loop synchronises
+  bool presized = false;
   // Split apply (P > 1 ranks, launch_ls_fold_union_label / launch_ls_zip): bucket k's spine and
   // zipper run only on its owner rank (k mod P), on zs, from copies of the bucket's refreshed
   // pairs and marks (two slots, by owned-bucket parity); every rank applies the union-find part.
@@ -993,7 +1035,8 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
                      uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr,
-                     const uint32_t* nsd = nullptr) {
+                     const uint32_t* nsd = nullptr, bool mid_p6 = false,
+                     bool ids_checked = false) {
   require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
@@ -1013,20 +1056,16 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   L.bitmap = (uint32_t*)sc.get("ls_bitmap", 2 * bm_words * 4);
   L.spq = (uint32_t*)sc.get("ls_spq", 2 * spq_words * 4);
   L.ws = (unsigned long long*)sc.get("ls_ws", 128);
-  if (knobs().kb_pick) {
-    L.anc = (uint32_t*)sc.get("ls_anchor", 2 * 4);
-    HIP_CHECK(hipMemsetAsync(L.anc, 0xFF, 2 * 4, s));
-    for (auto& e : L.pick_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (knobs().kb_gbits) {
-      L.gbits = (uint32_t*)sc.get("ls_gbits", bm_words * 4);
-      L.gx = (uint32_t*)sc.get("ls_gx", 2 * 4);
-      HIP_CHECK(hipMemsetAsync(L.gbits, 0, bm_words * 4, s));
-      HIP_CHECK(hipMemsetAsync(L.gx, 0xFF, 2 * 4, s));
-      // this rank's maps walk m records: the summary rule of tree_from_sorted
-      if (knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))
-        L.gsum = (uint32_t*)sc.get("ls_gsum", ((size_t)n_seq / 2048 + 2) * 4);
-    }
-  }
+  L.anc = (uint32_t*)sc.get("ls_anchor", 2 * 4);
+  HIP_CHECK(hipMemsetAsync(L.anc, 0xFF, 2 * 4, s));
+  for (auto& e : L.pick_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  L.gbits = (uint32_t*)sc.get("ls_gbits", bm_words * 4);
+  L.gx = (uint32_t*)sc.get("ls_gx", 2 * 4);
+  HIP_CHECK(hipMemsetAsync(L.gbits, 0, bm_words * 4, s));
+  HIP_CHECK(hipMemsetAsync(L.gx, 0xFF, 2 * 4, s));
+  // this rank's maps walk m records: the summary rule of tree_from_sorted
+  if (knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))
+    L.gsum = (uint32_t*)sc.get("ls_gsum", ((size_t)n_seq / 2048 + 2) * 4);
   launch_fill(L.parent, INV, n, s);
   launch_fill(L.jump, 0, n, s);
   launch_fill(L.hcnt, 0, n, s);
@@ -1067,14 +1106,19 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   uint16_t* digits = (uint16_t*)sc.get("ls_item_bins", mm * 2);
   const uint32_t* src = d_uv;
   const bool part = use_part(m);
+  // the second pass's records packed to 6 bytes for the direct edge pass (ids_checked: an id
+  // >= n_rank fails the caller anyway)
+  const bool pre6 = part && knobs().bin_direct && m > 0 && n_seq > 0 && ids_checked &&
+                    part_p6_ok(n_rank);
+  uint32_t* pws = nullptr;
   if (part) {
     if (part_done) {  // pass 1 ran beside the degree all-reduce and the sequence
-      uint32_t* pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
+      pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
       HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
-      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s);
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, mid_p6, pre6);
     } else {
-      uint32_t* pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
-      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false);
+      pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
+      launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false, pre6);
     }
     src = (const uint32_t*)items_b;
   }
@@ -1107,7 +1151,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     HIP_CHECK(hipMemsetAsync(ovf, 0, 4, s));
     uint64_t* binned = (uint64_t*)sc.get("ls_binned", std::max<uint64_t>(L.cstart[nb - 1], 1) * 8);
     launch_edge_bin(src, part, m, d_rank, n_rank, d_err, L.bins, nb, L.dseg + 512, L.dseg + 1024,
-                    binned, ovf, s);
+                    binned, ovf, s, pre6 ? pws : nullptr);
     std::vector<unsigned long long> cur(nb);
     HIP_CHECK(hipMemcpyAsync(cur.data(), L.dseg + 512, nb * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(L.h_pinned, ovf, 4, hipMemcpyDeviceToHost, s));
@@ -1120,6 +1164,10 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
       *nb_out = nb;
       return;
     }
+  }
+  if (pre6) {  // a bin overflowed: the scatter path reads unpacked records, so partition again
+    uint32_t* pws2 = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
+    launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws2, s, false, false);
   }
   unsigned long long* dstart = (unsigned long long*)sc.get("ls_bin_start", 513 * 8);
   L.sorted = group_by_bins(src, part, m, d_rank, n_rank, d_err, L.bins, nb, items, items_b, tmp,
@@ -1244,10 +1292,13 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
   if (solo) {
     kept = (uint64_t*)d_recv + L.ms;
   } else if (!L.split) {
-    // a larger kept buffer replaces one that earlier applies may still read: drain first
+    // a larger kept buffer replaces one that earlier applies (on s) may still read: drain s
+    // first.  multi_tree sizes it before its loop, so this only happens through the sheep_ls_*
+    // calls (their caller gives no bound)
     if (L.kept_bytes == 0) L.kept_bytes = L.scp->bytes_of("ls_kept_all");
     if (need > L.kept_bytes) {
-      HIP_CHECK(hipDeviceSynchronize());
+      if (L.presized) throw ApiError(-EIO, "lockstep: kept pairs beyond the pre-sized buffer");
+      HIP_CHECK(hipStreamSynchronize(s));
       L.kept_bytes = std::max(need, L.kept_bytes * 5 / 4);
     }
     kept = (uint64_t*)L.scp->get("ls_kept_all", L.kept_bytes);
@@ -1278,8 +1329,11 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     if (ne && k % L.P == L.rank) {
       const int z = L.nzip++ & 1;
       if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));  // the slot's last zipper
-      if (need > L.zkept_bytes[z]) {
-        HIP_CHECK(hipDeviceSynchronize());
+      if (need > L.zkept_bytes[z]) {  // (pre-sized by multi_tree: only via sheep_ls_*)
+        if (L.presized) throw ApiError(-EIO, "lockstep: kept pairs beyond the pre-sized buffer");
+        // the slot's last readers: the zipper on zs (waited for above) and the unpack on s
+        HIP_CHECK(hipStreamSynchronize(s));
+        HIP_CHECK(hipStreamSynchronize(L.zs));
         L.zkept_bytes[z] = std::max(need, L.zkept_bytes[z] * 5 / 4);
         L.zkept[z] = (uint64_t*)L.scp->get(z ? "ls_zkept1" : "ls_zkept0", L.zkept_bytes[z]);
       }
@@ -1398,6 +1452,19 @@ static uint32_t sequence_sharded(Ctx& c, Comm& comm, const uint32_t* deg_local, 
     comm.allgather_u64((const uint64_t*)(rank + (size_t)r * cs), (uint64_t*)rank, cs / 2, s);
     return 0;
   }
+  // The histograms over degree values are all-gathered: P x (max degree + 1) words.  When that
+  // is more than the degree slices themselves (a hub of high degree; or max degree 2^32 - 1,
+  // where max degree + 1 wraps), all-gather the slices instead and sort every id on every rank
+  // (maxdeg is the same on every rank here, so every rank takes the same branch).
+  if ((uint64_t)maxdeg + 1 > (uint64_t)cs) {
+    uint32_t* dall = (uint32_t*)sc.get("sq_deg_all", n_pad * 4);
+    comm.allgather_u64((const uint64_t*)dsl, (uint64_t*)dall, cs / 2, s);
+    uint32_t* nsd = (uint32_t*)sc.get("sq_nsd", (size_t)n_seq * 4);
+    const uint32_t n2 = sequence_dev(c, dall, n_ids, d_seq, rank, s, false, nsd);
+    if (n2 != n_seq) throw ApiError(-EIO, "sharded sequence: id counts disagree");
+    *nsd_out = nsd;
+    return n_seq;
+  }
   const uint32_t D = maxdeg + 1, Dp = D + (D & 1);
   // this rank's ids of degree > 0, sorted stably by degree (local ids: global - r c)
   const int passes = (bits_for(maxdeg) + 7) / 8;
@@ -1452,11 +1519,13 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   const bool yh = degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s, overlap,
                              overlap ? c.part_ev[0] : nullptr);
+  // packed first-pass records (an id >= n_ids fails this call: the degree pass's ERR_RANGE)
+  const bool mid6 = overlap && knobs().bin_direct && part_p6_ok(n_ids);
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
-    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh, mid6);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
     part_done = c.part_ev[1];
   }
@@ -1482,13 +1551,13 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   Lockstep L;
   L.ctx = &c;
   L.scp = &c.scratch;
-  L.defer = comm.size() == 1 && knobs().kb_defer != 0;
+  L.defer = comm.size() == 1;
   L.time_apply = false;
   c.ls_live++;
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
   ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done,
-           nsd);
+           nsd, mid6, true);
   if (part_done) HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));  // also when no tree is built
   check_err(c, s);
   uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);
@@ -1527,6 +1596,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     ls_set_split(L, (uint32_t)comm.rank(), (uint32_t)P, (uint64_t)P * cap_send);
   if (!L.split && P > 1)  // ls_apply's unpacked pairs, sized once
     (void)L.scp->get("ls_kept_all", (uint64_t)P * cap_send * 8);
+  L.presized = true;
   int64_t* d_cnt = (int64_t*)c.scratch.get("mt_cnt", 8);
   uint32_t caps[2] = {0, 0};
   hipEvent_t* exchanged = c.kb_ev;
@@ -1586,6 +1656,8 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   if (tm) tm->mark("pst");
   HIP_CHECK(hipStreamSynchronize(s));
   ls_timings(c, L);
+  // a walk guard or range error raised inside the bucket loop (maps, applies, zippers)
+  check_err_group(c, comm, s);
   return n_seq;
 }
 
@@ -1798,19 +1870,57 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
                             stats, s, [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
   }
   const bool overlap = !fused && ov != 0 && m > 0 && use_part(m);
+  // the first pass's records packed when the direct edge pass will read the second pass's
+  // (an id >= n_ids fails this call: the degree pass raises ERR_RANGE)
+  const bool mid6 = overlap && knobs().bin_direct && part_p6_ok(n_ids);
+  // Sampled capacities (from 2^25 records, the bucketed degree path, the first pass beside
+  // it): no counting read of the records — the degree scatter and the first partition pass
+  // write into capacity regions sized from a 1/256 sample (launch_degree_sampled).  A region
+  // that overflows sends the degrees (here, before the sequence reads them) or the partition
+  // (after the edge pass, with the hi bins' overflow) through the exact pass.
+  const bool sampled = mid6 && ov == 2 && m >= (1ull << 25) && 2 * m < (1ull << 32) &&
+                       knobs().degree != 1 && degs_tmp_words(m, n_ids) > 1;
+  // packed records the mid buffer holds (capacity regions: their largest possible sum)
+  const uint64_t mid_slots = sampled ? fs_room(m, 1024) : m;
+  uint32_t* ovf_deg = c.d_err + 2;
+  uint32_t* ovf_part = c.d_err + 3;
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
-  const bool yh = fused ? false
-                        : degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
-                                     overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
+  bool yh = false;
+  if (sampled) {
+    HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words
+    uint32_t* tmp = (uint32_t*)c.scratch.get("degs_tmp", degs_tmp_words(m, n_ids) * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
+    launch_degree_sampled(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, pws, mid_slots,
+                          stats, ovf_deg, s, c.part_ev[0]);
+  } else if (!fused) {
+    yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
+                    overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
+  }
   tm.mark(fused ? "degree_hist" : "degree");
   if (fused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
-  if (overlap) {
+  if (sampled) {
+    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m * 8, mid_slots * 6));
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
+    HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
+    const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench
+    launch_part_first_caps(d_uv, m, n_ids, mid, mid_slots, pws, ovf_part, c.side);
+    tm.span_end(sp, c.side);
+    HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
+    // the degrees are complete and valid unless a bucket outgrew its region (the stream syncs
+    // here once; sequence_dev would wait for the degree pass anyway)
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c.h_pinned[4]) {
+      degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, false, nullptr, stats);
+      tm.mark("degree_exact");
+    }
+  } else if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     if (ov != 2) HIP_CHECK(hipEventRecord(c.part_ev[0], s));
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench
-    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh, mid6);
     tm.span_end(sp, c.side);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
@@ -1823,6 +1933,10 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   DegInfo di;
   di.nsd = nsd;
   di.part_first_done = overlap || fused;
+  di.mid_p6 = mid6;
+  di.mid_slots = mid_slots;
+  di.mid_caps = sampled;
+  di.ids_checked = true;
   di.yhist_ready = yh;
   di.seq = d_seq;
   di.deg = deg;
@@ -2311,8 +2425,8 @@ int sheep_mpi_sequence(const uint32_t* edges_uv, uint64_t m, uint32_t n_ids, int
   comm.allreduce_max_i64(d_n, 2, s);
   HIP_CHECK(hipMemcpyAsync(hn, d_n, 16, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  if (hn[0] > (int64_t)0xFFFFFFFFll)
-    throw ApiError(-ERANGE, "mpi_sequence: vertex id 0xFFFFFFFF (INVALID) in the records");
+  if (hn[0] > (int64_t)0xFFFFFFFEll)  // as the other entry points: n_ids must stay below INVALID
+    throw ApiError(-ERANGE, "mpi_sequence: vertex id >= 0xFFFFFFFE in the records");
   n_ids = (uint32_t)hn[0];
   const uint64_t min_cap = (uint64_t)(-hn[1]);
   uint32_t* uv = upload_records(c, edges_uv, m, s);

@@ -40,30 +40,20 @@ struct Knobs {
   int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
                          //   after it (1), in line (0), fused into the degree scatter (3,
                          //   graph2tree_dev; taken anyway from 2^31 records)
-  int part_ysort = 1;    // SHEEP_PART_YSORT: the second partition pass orders each tile by y
-                         //   before its rank gathers (cache-line sharing)
-  int seq_sort = 2;      // SHEEP_SEQ_SORT: the sequence by a counting sort over degree classes (2),
-                         //   a radix sort of the ids with degree > 0 (1) or of all ids (0)
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
   int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)
   int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
-  int kb_refresh = 1;    // SHEEP_KB_REFRESH: re-resolve the kept starts before the zipper
-  int kb_gbits = 1;      // SHEEP_KB_GBITS: giant bitmap in front of the map's union-find
-  int kb_defer = 1;      // SHEEP_KB_DEFER: the map's union-find misses resolved by the refresh
-  int degb_plain = 1;    // SHEEP_DEGB_PLAIN: histogram adds without wave matching (bit 0: 64K
-                         //   buckets, bit 1: small buckets)
-  int degb_hist16 = 1;   // SHEEP_DEGB_HIST: one-read 64K-id histogram (0: two halves)
   int tree_stats = 0;    // SHEEP_TREE_STATS: 1 totals, 2 per bucket (stderr; diagnostics)
   int bin_direct = 1;    // SHEEP_BIN_DIRECT: the edge pass fills the hi bins directly (no scatter)
   int bin_slack = 50;    // SHEEP_BIN_SLACK: bin capacity = estimate x (1 + slack / 1000) + 8192
-  int kb_pick = 1;       // SHEEP_KB_PICK: the giant's anchor picked on the device (0: rank B0 - 1)
   int kb_gsum = -1;      // SHEEP_KB_GSUM: the map tests 64-rank "all in the giant" blocks in LDS
                          //   first; -1 auto (from 2^27 records), 0, 1
-  int kb_drop = 1;       // SHEEP_KB_DROP: the refresh drops in-bucket pairs of two marked ranks
   int ls_seq = 1;        // SHEEP_LS_SEQ: with P > 1 ranks each sorts the ids of its 1/P of the id
                          //   space (degrees reduce-scattered; 0: all-reduced, every rank sorts all)
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
                          //   rank (0: every rank applies every bucket's zipper)
+  int kb_merge = 0;      // SHEEP_KB_MERGE (lab): merge adjacent kb buckets while together they hold
+                         //   at most kb_merge / 10000 of the records (0: off)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
@@ -186,16 +176,37 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
                         unsigned long long* h_start = nullptr, hipEvent_t started = nullptr);
 // Partitioned rank gathers: uv (x, y) -> pre (x, rank[y] | sentinel) in x-digit order (mid:
 // m u64 scratch, ws: PART_WS_WORDS u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
-constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024;  // y / x digit counts, then u64 cursors
+// ws: y / x digit counts, the first pass's u64 cursors, the u32 region starts of both passes'
+// outputs, the second pass's cursors, the first pass's capacity region ends (sheep_kernels.hip).
+constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024;
+// p6: the records between the passes and after them are packed to 6 bytes (sheep_kernels.hip
+// "packed 6-byte records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
+bool part_p6_ok(uint32_t n_rank);
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
-                        bool yhist_ready = false);
+                        bool yhist_ready = false, bool p6 = false);
 // The two passes of launch_part_gather separately (the first needs no ranks, so it can run
 // while the sequence is sorted): uv -> mid (y-digit order), then mid -> pre (x-digit order).
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
-                       uint32_t* ws, hipStream_t s, bool yhist_ready);
+                       uint32_t* ws, hipStream_t s, bool yhist_ready, bool p6 = false);
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* pre, uint32_t* ws, hipStream_t s);
+                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool in6 = false,
+                        bool out6 = false, uint64_t mid_slots = 0, bool caps = false);
+// Sampled capacities (sheep_kernels.hip, "sampled capacities"): the degree pass without a
+// counting read — a 1/256 sample sizes each bucket's and each y digit's capacity region; the
+// y regions go to part_ws for launch_part_first_caps (packed records, mid_slots of them; the
+// event caps_done marks them written).  *ovf is set when a run outgrew its region: the degrees
+// are then invalid and the caller runs the exact pass.  False when not applicable.
+size_t degs_tmp_words(uint64_t m, uint32_t n_ids);
+// The most slots the sampled capacity regions of `items` items over n_regions can take (the
+// first pass's packed records: fs_room(m, 1024) slots of 6 bytes).
+uint64_t fs_room(uint64_t items, uint32_t n_regions);
+bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+                           uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
+                           uint32_t* part_ws, uint64_t mid_slots, uint32_t* stats, uint32_t* ovf,
+                           hipStream_t s, hipEvent_t caps_done);
+void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
+                            uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,
                            const uint32_t* selfc, int file_mode, const uint32_t* cnt, uint32_t* pst,
                            hipStream_t s,
@@ -213,10 +224,12 @@ struct KbSegs {
 // Direct binning (sheep_kernels.hip): records (uv, or k_part's pre records) -> items grouped by
 // hi bin, each bin in its capacity region [cursor[b] at entry, cap_end[b]); cursor[b] ends at
 // the bin's fill.  *ovf is set (and the run dropped) when a bin overflows its capacity.
+// part_ws (non-null only with pre): the records are launch_part_second's packed output, whose
+// x-digit regions part_ws holds.
 void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
                      uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
                      unsigned long long* cursor, const unsigned long long* cap_end, uint64_t* out,
-                     uint32_t* ovf, hipStream_t s);
+                     uint32_t* ovf, hipStream_t s, const uint32_t* part_ws = nullptr);
 // One kb bucket in two halves (sheep_kernels.hip): the map (records -> kept pairs + giant marks
 // + hi counts) and the apply (spine, zipper, union-find fold, labels).  counters: this
 // bucket parity's 4 words; anchor: see launch_kb_map.

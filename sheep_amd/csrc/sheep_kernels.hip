@@ -348,6 +348,14 @@ static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgro
 // runs).  part_ws layout (PART_WS_WORDS u32): y-digit counts [0, 1024), x-digit counts
 // [1024, 1280), u64 cursors from word 1280.
 static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_X = 1024, PW_CUR = 1280;
+// ...then the u32 region starts of both passes' outputs, the second pass's u64 cursors (the
+// first pass's stay: they are its regions' fill) and the first pass's capacity region ends.
+static constexpr uint32_t PW_YST = 1280 + 2 * 1024, PW_XST = PW_YST + PD_Y + 1;
+static constexpr uint32_t PW_XCUR = PW_XST + PD_X + 1, PW_YCAP = PW_XCUR + 2 * PD_X;
+static_assert(PW_XCUR % 2 == 0 && PW_YCAP % 2 == 0, "u64 arrays");
+// Second-pass records (x, ry): ry's sentinels.
+constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
+constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
 template <uint32_t ND>
 __device__ __forceinline__ uint32_t part_digit(uint32_t id, int sh) { return min(id >> sh, ND - 1); }
 static int part_shift(uint32_t n_rank, uint32_t nd) {  // id >> shift < nd for ids < n_rank
@@ -355,6 +363,77 @@ static int part_shift(uint32_t n_rank, uint32_t nd) {  // id >> shift < nd for i
   for (uint64_t v = n_rank ? n_rank - 1 : 0; v; v >>= 1) ++bits;
   for (uint32_t v = nd - 1; v; v >>= 1) ++db;
   return bits > db ? bits - db : 0;
+}
+
+// ---- packed 6-byte records (P6) ------------------------------------------------------------
+// Inside one digit region of a partition pass's output the digit's bits are implied, so with
+// every id below n_rank <= 2^26 a record needs 42 (first pass) or 43-45 (second pass) bits:
+//   first pass (by y digit, psh <= 16 low bits of y kept):  a = x,  b = y & (2^psh - 1);
+//   second pass (by x digit, shx <= 18 low bits of x kept): a = ry' << XH | x_lo >> 16,
+//                                                          b = x_lo & 0xFFFF,  XH = shx - 16,
+// ry' = ry, or a sentinel (RY_SELF / RY_OUT / INV) folded into the top of its 32 - XH bits.
+// A buffer of m records holds the u32 array a (4m bytes) then the u16 array b (2m bytes): the
+// three passes that write or read these records move 6 bytes per record instead of 8.  A
+// reader restores the digit from the region starts (k_part_cursor) of the position's region.
+// Only for callers where an id >= n_rank fails the call anyway (graph2tree_dev, the multi-rank
+// driver: the degree pass raises ERR_RANGE): such an id loses its high bits here.
+struct P6Ref {
+  const uint32_t* a;
+  const uint16_t* b;
+};
+__device__ __forceinline__ P6Ref p6_in(const void* base, uint64_t m) {
+  return {(const uint32_t*)base, (const uint16_t*)((const char*)base + 4 * m)};
+}
+__device__ __forceinline__ uint32_t p6_ry_enc(uint32_t ry, int xh) {
+  return ry >= RY_SELF ? ry & (~0u >> xh) : ry;  // sentinels to the top 3 values of 32 - xh bits
+}
+__device__ __forceinline__ uint32_t p6_ry_dec(uint32_t v, int xh) {
+  const uint32_t lim = (~0u >> xh) - 2u;
+  return v >= lim ? v | ~(~0u >> xh) : v;
+}
+
+// The digit of input position pos: the last region (of ND) whose start is <= pos (empty
+// regions share their start with the next one).  One full wave, two dependent loads: lane i
+// tests region i * (ND / 64), then lane i the i-th region of the segment found.
+template <uint32_t ND>
+__device__ __forceinline__ uint32_t wave_find_digit(const uint32_t* __restrict__ starts, uint64_t pos) {
+  constexpr uint32_t STEP = ND / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool ok1 = starts[lane * STEP] <= pos;
+  const uint64_t b1 = __ballot(ok1);
+  const uint32_t seg = 63 - __clzll((long long)(b1 | 1ull)) ;
+  const uint32_t i2 = seg * STEP + (lane < STEP ? lane : 0u);  // (in bounds for every lane)
+  const bool ok2 = lane < STEP && starts[i2] <= pos;
+  const uint64_t b2 = __ballot(ok2) | 1ull;
+  return seg * STEP + (63 - __clzll((long long)b2));
+}
+
+// A tile's regions [d0, d1] (the digits of its first and last input positions) in LDS: sst[0] =
+// d0, sst[1] = d1, sst[2 ..] = starts[d0 + 1 .. d1].  Called by every thread; ends in a barrier.
+template <uint32_t ND>
+__device__ __forceinline__ void tile_regions(const uint32_t* __restrict__ starts, uint64_t tb,
+                                             uint32_t tn, uint32_t* sst) {
+  if (threadIdx.x < 64) {
+    const uint32_t d0 = wave_find_digit<ND>(starts, tb);
+    const uint32_t d1 = wave_find_digit<ND>(starts, tb + tn - 1);
+    if (threadIdx.x == 0) { sst[0] = d0; sst[1] = d1; }
+  }
+  block_sync();
+  const uint32_t d0 = sst[0], d1 = sst[1];
+  for (uint32_t i = threadIdx.x; i < d1 - d0; i += blockDim.x) sst[2 + i] = starts[d0 + 1 + i];
+  block_sync();
+}
+// The digit of position pos of the tile (tile_regions above).
+__device__ __forceinline__ uint32_t tile_digit(const uint32_t* sst, uint64_t pos) {
+  uint32_t d = sst[0];
+  const uint32_t n = sst[1] - d;
+  if (n == 0) return d;
+  uint32_t lo = 0, cnt = n;  // entries sst[2 .. 2 + n) <= pos
+  while (cnt > 0) {
+    const uint32_t h = cnt >> 1;
+    if (sst[2 + lo + h] <= pos) { lo += h + 1; cnt -= h + 1; } else cnt = h;
+  }
+  return d + lo;
 }
 
 __global__ void __launch_bounds__(DEGB_THREADS)
@@ -449,13 +528,181 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
   }
 }
 
+// ---- sampled capacities (large inputs): no counting read of the records ------------------
+// The degree scatter and the first partition pass above need, before they write, where each
+// bucket's (y digit's) runs go: k_degb_count reads every record once for that (8 B per record,
+// 1.6 ms at RMAT-26, on the critical path: both chains wait for it).  Instead, every FS_STRIDE-th
+// record is counted (k_front_sample: 1/FS_STRIDE of the records), and each bucket / digit gets
+// a capacity region of its estimate plus six standard deviations of it plus a margin
+// (k_front_caps).  The scatter counts its chunk in LDS and reserves its runs with one atomic per
+// bucket (k_degb_scatter_cap); the histogram reads each region up to its fill; the partition
+// pass reserves on the digit cursors (k_part, cap_end).  A run that would cross its region's
+// end is dropped and a flag set: the caller then runs the exact (counted) pass instead.  The
+// regions and the fill are all the readers see, so any capacities give the same degrees.
+static constexpr uint32_t FS_STRIDE = 256;
+
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_front_sample(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
+               uint32_t NB, int psh, uint32_t* __restrict__ scnt /* NB, then PD_Y */) {
+  __shared__ uint32_t hb[DEGB_NB], hy[PD_Y];
+  for (uint32_t i = threadIdx.x; i < DEGB_NB; i += DEGB_THREADS) { hb[i] = 0; hy[i] = 0; }
+  block_sync();
+  const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
+  for (uint64_t k = (uint64_t)blockIdx.x * DEGB_THREADS + threadIdx.x; k < ns;
+       k += (uint64_t)gridDim.x * DEGB_THREADS) {
+    const uint2 e = uv[k * FS_STRIDE];
+    if (e.x >= n_ids || e.y >= n_ids) continue;  // the scatter reports it
+    atomicAdd(&hb[e.x >> SH], 1u);
+    if (file_mode || e.x != e.y) atomicAdd(&hb[e.y >> SH], 1u);
+    atomicAdd(&hy[part_digit<PD_Y>(e.y, psh)], 1u);
+  }
+  block_sync();
+  for (uint32_t i = threadIdx.x; i < NB; i += DEGB_THREADS)
+    if (hb[i]) atomicAdd(&scnt[i], hb[i]);
+  for (uint32_t i = threadIdx.x; i < PD_Y; i += DEGB_THREADS)
+    if (hy[i]) atomicAdd(&scnt[DEGB_NB + i], hy[i]);
+}
+
+// Capacity of a region estimated at est items from c samples (est = c * FS_STRIDE): est + 5
+// sigma (sigma = sqrt(FS_STRIDE * est), the sampling error) + 2048, at most lim.  A region
+// outgrows it with probability ~3e-7 on an unordered stream.  Over n regions the capacities
+// sum to at most E + 5 sqrt(FS_STRIDE n E) + 2048 n (Cauchy-Schwarz), E = the sampled total
+// <= 2 (m + FS_STRIDE) endpoints or m + FS_STRIDE records: fs_room sizes the buffers by it.
+__device__ __forceinline__ unsigned long long fs_cap(uint32_t c, unsigned long long lim) {
+  const double est = (double)c * FS_STRIDE;
+  const double cap = est + 5.0 * sqrt((double)FS_STRIDE * est) + 2048.0;
+  return cap < (double)lim ? (unsigned long long)cap : lim;
+}
+uint64_t fs_room(uint64_t items, uint32_t n_regions) {
+  const double e = (double)items + 2.0 * FS_STRIDE;
+  return (uint64_t)(e + 5.0 * std::sqrt((double)FS_STRIDE * n_regions * e)) + 2049ull * n_regions + 64;
+}
+
+// One block of 1024 threads: bucket regions (bst: NB + 1 starts, bcur: cursors = starts, bcap:
+// region ends) within ep_slots u16 entries, and the y-digit regions (ystart: PD_Y + 1 u32,
+// ycur: cursors, ycap: ends) within mid_slots records.  Regions that do not fit get capacity 0
+// (every run then overflows: the caller's exact pass takes over).
+__global__ void __launch_bounds__(1024)
+k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_t ep_slots,
+             uint64_t mid_slots, unsigned long long* bst, unsigned long long* bcur,
+             unsigned long long* bcap, uint32_t* ystart, unsigned long long* ycur,
+             unsigned long long* ycap) {
+  __shared__ unsigned long long ws[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint32_t n = pass ? PD_Y : NB;
+    const unsigned long long lim = pass ? m : 2 * m, room = pass ? mid_slots : ep_slots;
+    const unsigned long long c = (uint32_t)t < n ? fs_cap(scnt[(pass ? DEGB_NB : 0) + t], lim) : 0ull;
+    unsigned long long incl = c;  // inclusive wave scan (u64)
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) ws[w] = incl;
+    block_sync();
+    unsigned long long add = 0, total = 0;
+    for (int i = 0; i < 16; ++i) { if (i < w) add += ws[i]; total += ws[i]; }
+    const bool fits = total <= room;
+    const unsigned long long st = fits ? add + incl - c : 0ull, end = fits ? st + c : 0ull;
+    if ((uint32_t)t < n) {
+      if (pass) {
+        ystart[t] = (uint32_t)st;
+        ycur[t] = st;
+        ycap[t] = end;
+      } else {
+        bst[t] = st;
+        bcur[t] = st;
+        bcap[t] = end;
+      }
+    }
+    if (t == 0) {
+      if (pass) ystart[n] = (uint32_t)(fits ? total : 0ull);
+      else bst[n] = fits ? total : 0ull;
+    }
+    block_sync();
+  }
+}
+
+// k_degb_scatter on capacity regions: the chunk's bucket counts from LDS, its runs reserved on
+// the bucket cursors (bcur), dropped past the region end (bcap) with *ovf set.
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_degb_scatter_cap(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
+                   uint32_t NB, unsigned long long* bcur, const unsigned long long* __restrict__ bcap,
+                   uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc, uint32_t* ovf,
+                   uint32_t* err) {
+  __shared__ uint32_t cur[DEGB_NB], start[DEGB_NB], wsum[DEGB_THREADS / 64];
+  __shared__ unsigned long long goff[DEGB_NB];
+  __shared__ uint16_t buf[2 * DEGB_CHUNK];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t lmask = (1u << SH) - 1u;
+  constexpr int U = 8, RND = DEGB_CHUNK / (DEGB_THREADS * U);
+  for (uint32_t i = t; i < DEGB_NB; i += DEGB_THREADS) cur[i] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * DEGB_CHUNK;
+  const uint32_t cn = (uint32_t)min((uint64_t)DEGB_CHUNK, m - base);
+  uint2 ee[RND * U];  // the chunk stays in registers between the count and the placement
+#pragma unroll
+  for (int q = 0; q < RND * U; ++q) {
+    const uint32_t i = (uint32_t)q * DEGB_THREADS + t;
+    ee[q] = i < cn ? ld_rec_nt(uv + base + i) : make_uint2(INV, INV);
+  }
+  block_sync();
+#pragma unroll
+  for (int q = 0; q < RND * U; ++q) {
+    const uint2 e = ee[q];
+    if (e.x >= n_ids || e.y >= n_ids) {
+      if ((uint32_t)q * DEGB_THREADS + t < cn) atomicOr(err, ERR_RANGE);
+      continue;
+    }
+    atomicAdd(&cur[e.x >> SH], 1u);
+    if (file_mode || e.x != e.y) atomicAdd(&cur[e.y >> SH], 1u);
+  }
+  block_sync();
+  const uint32_t cnt = (uint32_t)t < NB ? cur[t] : 0u;
+  const uint32_t incl = wave_incl_scan(cnt);
+  if (lane == 63) wsum[w] = incl;
+  block_sync();
+  if ((uint32_t)t < NB) {
+    uint32_t add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    start[t] = add + incl - cnt;
+    cur[t] = add + incl - cnt;
+    unsigned long long g = ~0ull;
+    if (cnt) {
+      g = atomicAdd(&bcur[t], (unsigned long long)cnt);
+      if (g + cnt > bcap[t]) {
+        atomicOr(ovf, 1u);
+        g = ~0ull;
+      }
+    }
+    goff[t] = g;
+  }
+  block_sync();
+#pragma unroll
+  for (int q = 0; q < RND * U; ++q) {
+    const uint2 e = ee[q];
+    if (e.x >= n_ids || e.y >= n_ids) continue;
+    const bool loop = e.x == e.y;
+    buf[atomicAdd(&cur[e.x >> SH], 1u)] = (uint16_t)(e.x & lmask);
+    if (file_mode || !loop) buf[atomicAdd(&cur[e.y >> SH], 1u)] = (uint16_t)(e.y & lmask);
+    if (loop && selfc) atomicAdd(&selfc[e.x], 1u);
+  }
+  block_sync();
+  for (uint32_t b = w; b < NB; b += DEGB_THREADS / 64) {
+    const unsigned long long g = goff[b];
+    if (g == ~0ull) continue;
+    const uint32_t s0 = start[b], n = cur[b] - s0;
+    for (uint32_t j = lane; j < n; j += 64) ep[g + j] = buf[s0 + j];
+  }
+}
+
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
             uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
             uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
             const unsigned long long* __restrict__ bstart2 = nullptr,
-            const uint64_t* __restrict__ rec0 = nullptr) {
+            const uint64_t* __restrict__ rec0 = nullptr,
+            const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
@@ -472,6 +719,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
                    : bstart ? bstart[b + 1]
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
+  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[b]);  // (a region's fill past its end: dropped)
   if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
     const uint32_t lm = (1u << SH) - 1u;
     for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
@@ -509,7 +757,8 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
         uint64_t ik = i + k;
         uint32_t e = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
         bool done = !(ik >= s0 && ik < s1) || (H > 1 && (e >> 15) != h);
-        uint32_t v = H > 1 ? (e & (DEGB_HALF - 1)) : e;
+        // (masked: a capacity region's unwritten hole, read only on the way to the exact pass)
+        uint32_t v = H > 1 ? (e & (DEGB_HALF - 1)) : (e & (span - 1));
         if (plain) {  // as k_degb_hist16
           if (!done) atomicAdd(&cnt[v], 1u);
           continue;
@@ -552,7 +801,8 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
               uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
               uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
               const unsigned long long* __restrict__ bstart2 = nullptr,
-              const uint64_t* __restrict__ rec0 = nullptr) {
+              const uint64_t* __restrict__ rec0 = nullptr,
+              const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -565,10 +815,11 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
   const uint16_t* __restrict__ ep_s = sg ? ep2 : ep;
   const uint64_t last = (uint64_t)NB * nchunks - 1;
   const uint64_t s0 = sg ? bstart2[b] : bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
-  const uint64_t s1 = sg ? bstart2[b + 1]
-                         : bstart ? bstart[b + 1]
-                                  : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
-                                                 : (uint64_t)offsets[last] + counts[last];
+  uint64_t s1 = sg ? bstart2[b + 1]
+                   : bstart ? bstart[b + 1]
+                            : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
+                                           : (uint64_t)offsets[last] + counts[last];
+  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[b]);
   for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
     const uint64_t g1 = min(g0 + 65535, s1);
     for (uint32_t i = threadIdx.x; i < 32768; i += DEGB_THREADS) pk[i] = 0;
@@ -674,14 +925,13 @@ size_t degb_tmp_words(uint64_t m, uint32_t n_ids, int* SH_out, uint32_t* NB_out)
 }
 
 // deg (and selfc if non-null) for n_ids ids; tmp sized by degb_tmp_words.
-// k_degb_hist16 without the per-wave leader matching of repeated ids (SHEEP_DEGB_PLAIN=0
-// restores it): ids are spread over 65536 counters per bucket, so a wave rarely repeats one,
-// and the match cost more than the serialised hub adds it saves (RMAT-26 hist 11.7 -> 10.7 ms
-// of degree phase, twitter-shape 15.6 -> 14.1 ms).
-// bit 0: k_degb_hist16, bit 1: k_degb_hist.  The small-bucket histogram keeps the matching:
-// RMAT-22's 4096-id buckets repeat hub ids within a wave (degree 0.88 -> 0.94 ms plain), the
-// LJ shape gains (0.81 -> 0.72 ms).
-static int degb_plain() { return knobs().degb_plain; }
+// k_degb_hist16 adds without the per-wave leader matching of repeated ids: ids are spread over
+// 65536 counters per bucket, so a wave rarely repeats one, and the match cost more than the
+// serialised hub adds it saves (RMAT-26 hist 11.7 -> 10.7 ms of degree phase, twitter-shape
+// 15.6 -> 14.1 ms).  The small-bucket histogram (k_degb_hist) keeps the matching: RMAT-22's
+// 4096-id buckets repeat hub ids within a wave (degree 0.88 -> 0.94 ms plain); the LJ shape
+// would gain (0.81 -> 0.72 ms).
+static constexpr int DEGB_PLAIN16 = 1, DEGB_PLAIN_SMALL = 0;
 
 bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                             uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
@@ -728,15 +978,67 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   hipLaunchKernelGGL(k_degb_scatter, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
                      n_ids, file_mode, SH, NB, (const uint32_t*)counts, (const uint32_t*)offsets,
                      nchunks, ep, selfc, tm);
-  if (H > 1 && knobs().degb_hist16)
+  if (H > 1)
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
-                       (const unsigned long long*)bstart, stats, degb_plain() & 1);
+                       (const unsigned long long*)bstart, stats, DEGB_PLAIN16);
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
-                       deg, (const unsigned long long*)bstart, stats, degb_plain() >> 1);
+                       deg, (const unsigned long long*)bstart, stats, DEGB_PLAIN_SMALL);
   return yhist != nullptr;
+}
+
+// The sampled-capacity degree pass (see k_front_sample): scratch layout in u32 words.
+static uint64_t degs_ep_slots(uint64_t m, uint32_t NB) { return fs_room(2 * m, NB); }
+size_t degs_tmp_words(uint64_t m, uint32_t n_ids) {
+  int SH = 0;
+  uint32_t NB = 0;
+  if (!degb_params(n_ids, &SH, &NB)) return 1;
+  // samples (2 x 1024), bucket starts / cursors / ends (u64), the u16 entries (+16-B pad)
+  return 2 * DEGB_NB + 2 * (3 * (size_t)DEGB_NB + 2) + (degs_ep_slots(m, NB) + 1) / 2 + 16;
+}
+
+bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+                           uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
+                           uint32_t* part_ws, uint64_t mid_slots, uint32_t* stats, uint32_t* ovf,
+                           hipStream_t s, hipEvent_t caps_done) {
+  int SH;
+  uint32_t NB;
+  if (m == 0 || n_ids == 0 || !degb_params(n_ids, &SH, &NB) || 2 * m >= (1ull << 32)) return false;
+  uint32_t* scnt = tmp;
+  unsigned long long* bst = (unsigned long long*)(tmp + 2 * DEGB_NB);
+  unsigned long long* bcur = bst + DEGB_NB + 1;
+  unsigned long long* bcap = bcur + DEGB_NB;
+  uint16_t* ep = (uint16_t*)(((uintptr_t)(bcap + DEGB_NB + 1) + 15) & ~(uintptr_t)15);
+  if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  (void)hipMemsetAsync(scnt, 0, 2 * DEGB_NB * 4, s);
+  const int psh = part_shift(n_ids, PD_Y);  // the first partition pass's y digits
+  const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
+  const unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
+  hipLaunchKernelGGL(k_front_sample, dim3(sg), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m, n_ids,
+                     file_mode, SH, NB, psh, scnt);
+  hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
+                     degs_ep_slots(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST,
+                     (unsigned long long*)(part_ws + PW_CUR), (unsigned long long*)(part_ws + PW_YCAP));
+  if (caps_done) (void)hipEventRecord(caps_done, s);
+  const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
+  hipLaunchKernelGGL(k_degb_scatter_cap, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
+                     n_ids, file_mode, SH, NB, bcur, (const unsigned long long*)bcap, ep, selfc, ovf, err);
+  if (SH > 15)
+    hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, n_ids, deg,
+                       (const unsigned long long*)bst, stats, DEGB_PLAIN16, (const uint16_t*)nullptr,
+                       (const unsigned long long*)nullptr, (const uint64_t*)nullptr,
+                       (const unsigned long long*)bcur);
+  else
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, SH, 1u, n_ids,
+                       deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
+                       (const uint16_t*)nullptr, (const unsigned long long*)nullptr,
+                       (const uint64_t*)nullptr, (const unsigned long long*)bcur);
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -918,7 +1220,6 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
   int SH;
   uint32_t NB;
   if (m == 0 || n_ids == 0 || !degb_params(n_ids, &SH, &NB)) return false;
-  if (SH > 15 && !knobs().degb_hist16) return false;
   const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   const uint64_t cw = (uint64_t)NB * nchunks;
   const uint64_t gw = (uint64_t)NB * ((nchunks + TM_G - 1) / TM_G);
@@ -949,12 +1250,12 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
   if (SH > 15)
     hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)nullptr,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, n_ids, deg,
-                       (const unsigned long long*)by, stats, degb_plain() & 1,
+                       (const unsigned long long*)by, stats, DEGB_PLAIN16,
                        (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
   else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)nullptr,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, SH, 1u,
-                       n_ids, deg, (const unsigned long long*)by, stats, degb_plain() >> 1,
+                       n_ids, deg, (const unsigned long long*)by, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
   return true;
 }
@@ -1664,9 +1965,6 @@ void launch_chunk_degsum(const uint32_t* seq, const uint32_t* deg, uint32_t n_se
 // any (keep many gathers in flight).  pst (nullable) as in k_edge_pass.
 // PRE: the records are k_part's output (x, ry): rank[y] was gathered already (or is one of the
 // sentinels RY_SELF / RY_OUT), only rank[x] is gathered here.
-constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
-constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
-
 // TM: the tile histograms are written tile-major (bin_sort_u64's k_tm_* passes).
 template <int DB, bool PRE, bool BINS = false, bool TM = false>
 __global__ void __launch_bounds__(RS_THREADS)
@@ -1784,28 +2082,73 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // item (self-loops, INVALID hi) are not stored.  Tile = NT threads x IT records, staged in LDS
 // in bin order and written as whole runs per wave (as k_bin_scatter).
 // ---------------------------------------------------------------------------------------
-template <bool PRE, int NT, int IT>
+// Largest i with tb[i] <= v over a 512-entry table (entries past the used ones hold INV, and
+// v < INV): nine halvings with a fixed trip count, so the searches of a thread's N values
+// interleave (N LDS loads in flight per step, not one dependent chain per value).
+template <int N>
+__device__ __forceinline__ void search512(const uint32_t* tb, const uint32_t* v, uint32_t* idx) {
+  uint32_t lo[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) lo[k] = 0;
+#pragma unroll
+  for (uint32_t half = 256; half; half >>= 1) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (tb[lo[k] + half] <= v[k]) lo[k] += half;
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) idx[k] = lo[k];
+}
+
+// IN6 (with PRE): the records are k_part<1>'s packed output; x's digit bits come from the
+// x-digit region starts xst (shx: the digit shift).
+template <bool PRE, int NT, int IT, bool IN6 = false>
 __global__ void __launch_bounds__(NT)
 k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
            uint32_t n_rank, uint32_t* err, const uint32_t* __restrict__ bins, uint32_t nb,
            unsigned long long* cursor, const unsigned long long* __restrict__ cap_end,
-           uint64_t* __restrict__ out, uint32_t* ovf) {
+           uint64_t* __restrict__ out, uint32_t* ovf, const uint32_t* __restrict__ xst, int shx) {
   static_assert(NT >= 512, "one thread per bin in the scan");
+  static_assert(!IN6 || PRE, "packed records are second-pass records");
   constexpr int TILE = NT * IT;
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[512], tstart[512], sb[512], wsum[NT / 64];
   __shared__ unsigned long long gbase[512];
+  __shared__ uint32_t sst[IN6 ? PD_X + 2 : 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
   const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
-  if (t < 512) hist[t] = 0;
-  for (uint32_t i = t; i < nb; i += NT) sb[i] = bins[i];
+  if (t < 512) {
+    hist[t] = 0;
+    sb[t] = (uint32_t)t < nb ? bins[t] : INV;  // padded: search512
+  }
   uint2 e[IT];
   uint32_t rx[IT], ry[IT];
+  if (IN6) {
+    const P6Ref pin = p6_in(uv, m);
+    const int xh = shx > 16 ? shx - 16 : 0;
+    uint32_t ea[IT];
+    uint16_t eb[IT];
 #pragma unroll
-  for (int k = 0; k < IT; ++k) {
-    const uint32_t j = (uint32_t)k * NT + t;
-    e[k] = j < tile_n ? uv[tbase + j] : make_uint2(0, PRE ? RY_SELF : 0u);
+    for (int k = 0; k < IT; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      ea[k] = j < tile_n ? pin.a[tbase + j] : 0u;
+      eb[k] = j < tile_n ? pin.b[tbase + j] : (uint16_t)0;
+    }
+    tile_regions<PD_X>(xst, tbase, tile_n, sst);  // (the loads above are in flight)
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      const uint32_t xlo = ((ea[k] & ((1u << xh) - 1u)) << 16) | eb[k];
+      const uint32_t x = (tile_digit(sst, tbase + min(j, tile_n - 1)) << shx) | xlo;
+      e[k] = j < tile_n ? make_uint2(x, p6_ry_dec(ea[k] >> xh, xh)) : make_uint2(0, RY_SELF);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      e[k] = j < tile_n ? uv[tbase + j] : make_uint2(0, PRE ? RY_SELF : 0u);
+    }
   }
 #pragma unroll
   for (int k = 0; k < IT; ++k) {  // every gather issued before any is used
@@ -1819,12 +2162,11 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
   }
   block_sync();
   uint64_t item[IT];
-  uint32_t pk[IT];  // bin << 16 | index within the tile's run of the bin; ~0u: not stored
+  uint32_t hiv[IT], pk[IT];  // pk: bin << 16 | index within the tile's run of the bin; ~0u: not stored
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     const bool loop = PRE ? e[k].y == RY_SELF : e[k].x == e[k].y;
     uint32_t hi = INV, lo = INV;
-    pk[k] = ~0u;
     if ((uint32_t)k * NT + t < tile_n && !loop) {  // insert's edge loop, jtree.cpp:73-90
       const bool ox = e[k].x >= n_rank;
       bool oy;
@@ -1839,11 +2181,12 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
       }
     }
     item[k] = ((uint64_t)hi << 32) | lo;
-    if (hi != INV) {
-      const uint32_t d = bin_of(sb, nb, hi);
-      pk[k] = (d << 16) | atomicAdd(&hist[d], 1u);
-    }
+    hiv[k] = hi == INV ? 0u : hi;  // searched anyway (no divergence), not stored
   }
+  search512<IT>(sb, hiv, pk);
+#pragma unroll
+  for (int k = 0; k < IT; ++k)
+    pk[k] = (uint32_t)(item[k] >> 32) != INV ? (pk[k] << 16) | atomicAdd(&hist[pk[k]], 1u) : ~0u;
   block_sync();
   if (t < 512) {
     const uint32_t c = hist[t];
@@ -1871,27 +2214,33 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
   for (int k = 0; k < IT; ++k)
     if (pk[k] != ~0u) stage[tstart[pk[k] >> 16] + (pk[k] & 0xFFFFu)] = item[k];
   block_sync();
-  for (uint32_t d = w; d < 512; d += NT / 64) {
-    const uint32_t c = hist[d];
+  // The staged tile in bin order, written with every lane busy: slot j belongs to the last bin
+  // whose start is <= j (empty bins share their start with the next one).  (One wave per bin
+  // run left 3/4 of the lanes idle on ~16-item runs: 2x the LDS and store instructions.)
+  const uint32_t n_st = tstart[511] + hist[511];
+  for (uint32_t j = t; j < n_st; j += NT) {
+    uint32_t d;
+    search512<1>(tstart, &j, &d);
     const unsigned long long g = gbase[d];
-    if (c == 0 || g == ~0ull) continue;
-    const uint32_t s0 = tstart[d];
-    for (uint32_t j = lane; j < c; j += 64) out[g + j] = stage[s0 + j];
+    if (g != ~0ull) out[g + (j - tstart[d])] = stage[j];
   }
 }
 
 void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* rank,
                      uint32_t n_rank, uint32_t* err, const uint32_t* bins, uint32_t nb,
                      unsigned long long* cursor, const unsigned long long* cap_end, uint64_t* out,
-                     uint32_t* ovf, hipStream_t s) {
+                     uint32_t* ovf, hipStream_t s, const uint32_t* part_ws) {
   if (m == 0) return;
   // 8192-record tiles, 64 KB stage: two blocks of 16 waves per CU (RMAT-26 edge phase: 512 x
   // 16 -> 8.9 ms, 1024 x 16 -> 10.8, 512 x 8 -> 8.5, 1024 x 8 -> 7.8)
   constexpr int NT = 1024, IT = 8;
   const unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
-  auto k = pre ? k_edge_bin<true, NT, IT> : k_edge_bin<false, NT, IT>;
+  const bool in6 = pre && part_ws;
+  auto k = in6 ? k_edge_bin<true, NT, IT, true>
+               : pre ? k_edge_bin<true, NT, IT> : k_edge_bin<false, NT, IT>;
   hipLaunchKernelGGL(k, dim3(nt), dim3(NT), 0, s, (const uint2*)uv, m, rank, n_rank, err, bins, nb,
-                     cursor, cap_end, out, ovf);
+                     cursor, cap_end, out, ovf, in6 ? part_ws + PW_XST : (const uint32_t*)nullptr,
+                     part_shift(n_rank, PD_X));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1931,47 +2280,97 @@ k_part_count(const uint2* __restrict__ uv, uint64_t m, int sh, uint32_t* __restr
 }
 
 // cursor[d] = exclusive prefix of hist (one block of ND threads); hist is then cleared.
+// starts (nullable): the same prefix as u32, ND + 1 entries (the last = the total) — the digit
+// regions of this pass's output, which a packed (P6) reader needs to restore the digit bits.
 template <uint32_t ND>
-__global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor) {
-  __shared__ unsigned long long s[ND];
+__global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32_t* starts) {
+  __shared__ unsigned long long s[ND + 1];
   uint32_t t = threadIdx.x;
   s[t] = hist[t];
   block_sync();
   if (t == 0) {
     unsigned long long run = 0;
     for (uint32_t i = 0; i < ND; ++i) { unsigned long long v = s[i]; s[i] = run; run += v; }
+    s[ND] = run;
   }
   block_sync();
   cursor[t] = s[t];
+  if (starts) {
+    starts[t] = (uint32_t)s[t];
+    if (t == 0) starts[ND] = (uint32_t)s[ND];
+  }
   hist[t] = 0;
 }
 
 // ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1), ND / NT per thread in the scan.
 // MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
-template <int MODE, int NT, int IT, uint32_t ND>
+// in, m: the input and its positions.  IN6 (MODE 1): the input is the first pass's P6 output
+// (m slots): y's digit from the region starts in_starts (psh = ish), which end at
+// in_starts[PD_Y]; a position counts only below its region's fill (in_fill, capped at in_cap:
+// capacity regions leave gaps).  OUT6: the output is written as P6 records, m_out slots.
+// cap_end / ovf (nullable, MODE 0): capacity regions — a run past its digit's end is dropped
+// and *ovf set.
+template <int MODE, int NT, int IT, uint32_t ND, bool IN6 = false, bool OUT6 = false>
 __global__ void __launch_bounds__(NT)
-k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
+k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, uint64_t m_out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
-       const uint32_t* __restrict__ rank, uint32_t n_rank, int ysh) {
+       const uint32_t* __restrict__ rank, uint32_t n_rank, int ysh,
+       const uint32_t* __restrict__ in_starts, int ish,
+       const unsigned long long* __restrict__ in_fill, const unsigned long long* __restrict__ in_cap,
+       const unsigned long long* __restrict__ cap_end, uint32_t* ovf) {
   static_assert(ND % NT == 0 || NT % ND == 0, "digits per thread");
+  static_assert(!IN6 || MODE == 1, "packed input: the second pass only");
+  static_assert(IT <= 32, "validity mask");
   constexpr int R = ND > (uint32_t)NT ? (int)ND / NT : 1;  // digits per thread in the scan
   constexpr int PT_ITEMS = IT;
   constexpr int TILE = NT * PT_ITEMS;
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[ND], tstart[ND], hx[MODE == 0 ? PD_X : 1], wsum[NT / 64];
   __shared__ unsigned long long gbase[ND];
+  __shared__ uint32_t sst[IN6 ? PD_Y + 2 : 1], sfill[IN6 ? PD_Y : 1], s_nv;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
-  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
+  const uint64_t lim = IN6 ? min(m, (uint64_t)in_starts[PD_Y]) : m;
+  if (tbase >= lim) return;  // (the grid covers m slots; the regions may end earlier)
+  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, lim - tbase);
   for (uint32_t i = t; i < ND; i += NT) hist[i] = 0;
   if (MODE == 0)
     for (uint32_t i = t; i < PD_X; i += NT) hx[i] = 0;
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
+  uint32_t vm = 0;  // bit k: item k is a record
+  if (IN6) {
+    const P6Ref pin = p6_in(in, m);
+    uint32_t ya[PT_ITEMS];
+    uint16_t yb[PT_ITEMS];
 #pragma unroll
-  for (int k = 0; k < PT_ITEMS; ++k) {
-    uint32_t j = (uint32_t)k * NT + t;
-    rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      ya[k] = j < tile_n ? pin.a[tbase + j] : 0u;
+      yb[k] = j < tile_n ? pin.b[tbase + j] : (uint16_t)0;
+    }
+    tile_regions<PD_Y>(in_starts, tbase, tile_n, sst);  // (the loads above are in flight)
+    const uint32_t d0 = sst[0];
+    for (uint32_t i = t; i <= sst[1] - d0; i += NT) {
+      const unsigned long long f = in_fill[d0 + i], c = in_cap ? in_cap[d0 + i] : f;
+      sfill[i] = (uint32_t)min(f, c);
+    }
+    block_sync();
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      const uint64_t pos = tbase + min(j, tile_n - 1);
+      const uint32_t d = tile_digit(sst, pos);
+      rec[k] = ((uint64_t)((d << ish) | yb[k]) << 32) | ya[k];
+      vm |= (uint32_t)(j < tile_n && pos < sfill[d - d0]) << k;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      uint32_t j = (uint32_t)k * NT + t;
+      rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+      vm |= (uint32_t)(j < tile_n) << k;
+    }
   }
   if (MODE == 1 && ysh >= 0) {
     // The tile in y order first, by 256 sub-ranges of its y digit (counting sort in LDS): the
@@ -1981,7 +2380,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
     block_sync();
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k)
-      if ((uint32_t)k * NT + t < tile_n) li[k] = atomicAdd(&hist[(uint32_t)(rec[k] >> (32 + ysh)) & 255u], 1u);
+      if ((vm >> k) & 1) li[k] = atomicAdd(&hist[(uint32_t)(rec[k] >> (32 + ysh)) & 255u], 1u);
     block_sync();
     if (t < 256) {
       const uint32_t c = hist[t], incl = wave_incl_scan(c);
@@ -1993,18 +2392,22 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
       uint32_t add = 0;
       for (int i = 0; i < w; ++i) add += wsum[i];
       tstart[t] += add;
+      if (t == 255) s_nv = tstart[t] + hist[t];
       hist[t] = 0;
     }
     block_sync();
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k)
-      if ((uint32_t)k * NT + t < tile_n)
+      if ((vm >> k) & 1)
         stage[tstart[(uint32_t)(rec[k] >> (32 + ysh)) & 255u] + li[k]] = rec[k];
     block_sync();
+    const uint32_t n_valid = s_nv;
+    vm = 0;
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
-      rec[k] = j < tile_n ? stage[j] : 0ull;
+      rec[k] = j < n_valid ? stage[j] : 0ull;
+      vm |= (uint32_t)(j < n_valid) << k;
     }
   }
   if (MODE == 1) {  // (x, y) -> (x, ry)
@@ -2024,7 +2427,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   block_sync();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
-    if ((uint32_t)k * NT + t < tile_n) {
+    if ((vm >> k) & 1) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
       li[k] = atomicAdd(&hist[part_digit<ND>(key, sh)], 1u);
       if (MODE == 0) atomicAdd(&hx[part_digit<PD_X>((uint32_t)rec[k], shx)], 1u);
@@ -2043,7 +2446,12 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
       const uint32_t d = t * R + r;
       tstart[d] = run;
       run += c[r];
-      gbase[d] = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
+      unsigned long long g = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
+      if (cap_end && c[r] && g + c[r] > cap_end[d]) {  // past the digit's capacity: dropped
+        atomicOr(ovf, 1u);
+        g = ~0ull;
+      }
+      gbase[d] = g;
     }
   }
   if (MODE == 0)
@@ -2059,22 +2467,44 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out,
   block_sync();
 #pragma unroll
   for (int k = 0; k < PT_ITEMS; ++k) {
-    if ((uint32_t)k * NT + t < tile_n) {
+    if ((vm >> k) & 1) {
       uint32_t key = MODE == 0 ? (uint32_t)(rec[k] >> 32) : (uint32_t)rec[k];
       stage[tstart[part_digit<ND>(key, sh)] + li[k]] = rec[k];
     }
   }
   block_sync();
-  for (uint32_t j = t; j < tile_n; j += NT) {
+  uint32_t* oa = (uint32_t*)out;
+  uint16_t* ob = (uint16_t*)((char*)out + 4 * m_out);
+  const int xh = shx > 16 ? shx - 16 : 0;  // MODE 1, OUT6: x bits above the u16 half
+  const uint32_t n_st = tstart[ND - 1] + hist[ND - 1];  // the staged records
+  for (uint32_t j = t; j < n_st; j += NT) {
     uint64_t r = stage[j];
     uint32_t d = part_digit<ND>(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
-    out[gbase[d] + (j - tstart[d])] = r;
+    if (gbase[d] == ~0ull) continue;
+    const uint64_t pos = gbase[d] + (j - tstart[d]);
+    if (!OUT6) {
+      out[pos] = r;
+    } else if (MODE == 0) {  // a = x, b = y's low sh bits
+      oa[pos] = (uint32_t)r;
+      ob[pos] = (uint16_t)((uint32_t)(r >> 32) & ((1u << sh) - 1u));
+    } else {  // a = ry' << xh | x_lo >> 16, b = x_lo & 0xFFFF
+      // (masked: an id >= n_rank, clamped to the last digit, must not spill into ry's bits)
+      const uint32_t xlo = ((uint32_t)r - (d << sh)) & ((1u << sh) - 1u);
+      oa[pos] = (p6_ry_enc((uint32_t)(r >> 32), xh) << xh) | (xlo >> 16);
+      ob[pos] = (uint16_t)(xlo & 0xFFFFu);
+    }
   }
 }
 
+// Whether the partition passes may use packed records: every digit region's low bits fit.
+bool part_p6_ok(uint32_t n_rank) {
+  return n_rank > 0 && part_shift(n_rank, PD_Y) <= 16 && part_shift(n_rank, PD_X) <= 18;
+}
+
 // uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: PART_WS_WORDS.
+// p6: mid is written packed (the second pass then reads it packed).
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
-                       uint32_t* ws, hipStream_t s, bool yhist_ready) {
+                       uint32_t* ws, hipStream_t s, bool yhist_ready, bool p6) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   uint32_t* yhist = ws;
@@ -2086,31 +2516,62 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
     (void)hipMemsetAsync(ws, 0, PW_CUR * 4, s);
     hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
   }
-  hipLaunchKernelGGL(k_part_cursor<PD_Y>, dim3(1), dim3(PD_Y), 0, s, yhist, cursor);
+  hipLaunchKernelGGL(k_part_cursor<PD_Y>, dim3(1), dim3(PD_Y), 0, s, yhist, cursor, ws + PW_YST);
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
-  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt), dim3(PT0_THREADS),
-                     0, s, (const uint64_t*)uv, m, mid, cursor, xhist, sh, shx,
-                     (const uint32_t*)nullptr, n_rank, -1);
+  auto k = p6 ? k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, true>
+              : k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m, mid, m,
+                     cursor, xhist, sh, shx, (const uint32_t*)nullptr, n_rank, -1,
+                     (const uint32_t*)nullptr, 0, (const unsigned long long*)nullptr,
+                     (const unsigned long long*)nullptr, (const unsigned long long*)nullptr,
+                     (uint32_t*)nullptr);
 }
 
-void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* pre, uint32_t* ws, hipStream_t s) {
+// The first pass into the capacity regions launch_degree_sampled left in ws (packed records,
+// mid_slots of them in mid); a run past its region's end is dropped and *ovf set.
+void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
+                            uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s) {
   if (m == 0) return;
-  const int shx = part_shift(n_rank, PD_X);
-  const int ysh = knobs().part_ysort ? std::max(part_shift(n_rank, PD_Y) - 8, 0) : -1;
+  const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
+  (void)hipMemsetAsync(ws + PW_X, 0, PD_X * 4, s);
+  uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, true>), dim3((unsigned)nt),
+                     dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m, mid, mid_slots,
+                     (unsigned long long*)(ws + PW_CUR), ws + PW_X, sh, shx, (const uint32_t*)nullptr,
+                     n_rank, -1, (const uint32_t*)nullptr, 0, (const unsigned long long*)nullptr,
+                     (const unsigned long long*)nullptr,
+                     (const unsigned long long*)(ws + PW_YCAP), ovf);
+}
+
+// in6: mid holds the first pass's packed records (mid_slots of them: the capacity regions'
+// positions, else m; caps: capacity regions, bounded by their ends); out6: pre is written packed.
+void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
+                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool in6, bool out6,
+                        uint64_t mid_slots, bool caps) {
+  if (m == 0) return;
+  const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
+  const int ysh = std::max(sh - 8, 0);
   uint32_t* xhist = ws + PW_X;
-  unsigned long long* cursor = (unsigned long long*)(ws + PW_CUR);
-  hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor);
-  uint64_t nt = (m + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
-  hipLaunchKernelGGL((k_part<1, PT1_THREADS, PT1_ITEMS, PD_X>), dim3((unsigned)nt), dim3(PT1_THREADS),
-                     0, s, mid, m, pre, cursor, xhist, shx, shx, rank, n_rank, ysh);
+  unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
+  hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
+  const uint64_t pos = in6 && mid_slots ? mid_slots : m;
+  uint64_t nt = (pos + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
+  auto k = in6 ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
+                       : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, false>)
+               : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>
+                       : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, false>);
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, pos, pre, m, cursor, xhist,
+                     shx, shx, rank, n_rank, ysh, (const uint32_t*)(ws + PW_YST), sh,
+                     (const unsigned long long*)(ws + PW_CUR),
+                     caps ? (const unsigned long long*)(ws + PW_YCAP) : (const unsigned long long*)nullptr,
+                     (const unsigned long long*)nullptr, (uint32_t*)nullptr);
 }
 
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
-                        bool yhist_ready) {
-  launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready);
-  launch_part_second(mid, m, rank, n_rank, pre, ws, s);
+                        bool yhist_ready, bool p6) {
+  launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready, p6);
+  launch_part_second(mid, m, rank, n_rank, pre, ws, s, p6, p6, m, false);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3217,7 +3678,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                          uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc,
-                         knobs().kb_drop);
+                         1);
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL((k_kb_spine<true, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
@@ -3252,7 +3713,7 @@ void launch_kb_refresh(uint64_t* kept, const uint32_t* n_kept, uint32_t* uf, con
                        const uint32_t* gx, const uint32_t* anc, hipStream_t s) {
   if (!gx) gbits = nullptr;
   hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, n_kept, uf, label, bitmap,
-                     B0, anchor, gbits, gx, anc, knobs().kb_drop);
+                     B0, anchor, gbits, gx, anc, 1);
 }
 
 // ---- split lockstep apply (P ranks; sheep_capi.cpp ls_apply) ------------------------------

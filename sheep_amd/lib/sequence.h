@@ -45,8 +45,8 @@ std::vector<vid_t> mpiSequence(GraphType const& graph) {
   uint32_t n_seq = 0;
   int rc = sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
                               SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq);
-  if (rc == -ERANGE && n_seq > seq.size()) {
-    seq.resize(n_seq);
+  if (rc == -ERANGE && n_seq > 0) {  // on every rank, also those whose buffer was large enough
+    seq.resize(std::max<size_t>(seq.size(), n_seq));
     rc = sheep_mpi_sequence(graph.records_data(), graph.records(), graph.getMaxVid(),
                             SHEEP_DEGREE_LLAMA, seq.data(), (uint32_t)seq.size(), &n_seq);
   }

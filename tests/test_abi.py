@@ -68,10 +68,13 @@ def test_options_read_once_and_settable_without_gpu():
 
     old = capi.set_option("kb_buckets", 7)
     assert capi.set_option("kb_buckets", old) == 7
-    for name in ("ls_split", "ls_seq", "seq_sort", "part_ysort"):  # options added in round 3
+    for name in ("ls_split", "ls_seq"):  # options added in round 3
         v = capi.set_option(name, 0)
         assert capi.set_option(name, v) == 0
-    for gone in ("sort", "bin_tm", "bin_scatter", "ep_plain", "seq_compact"):  # removed in round 3
+    # removed in round 3, then in round 4 the A/B-only ones (always on now)
+    for gone in ("sort", "bin_tm", "bin_scatter", "ep_plain", "seq_compact", "seq_sort",
+                 "part_ysort", "kb_refresh", "kb_gbits", "kb_defer", "degb_plain", "degb_hist",
+                 "kb_pick", "kb_drop"):
         with pytest.raises(capi.SheepError):
             capi.set_option(gone, 0)
     with pytest.raises(capi.SheepError):

@@ -103,16 +103,14 @@ def _degrees(case, rng):
     return d
 
 
-@pytest.mark.parametrize("seq_sort", [2, 1, 0])
 @pytest.mark.parametrize("case", ["heavy", "small", "ones", "zeros", "full", "one"])
-def test_sequence_from_degrees(oracle, gpu, options, seq_sort, case):
+def test_sequence_from_degrees(oracle, gpu, case):
     """sheep_sequence_dev on crafted degree vectors (sequence.h:55-61: degree > 0, by degree,
-    ties in id order) under each sort: the counting sort's classes below 1024 and the radix-
-    sorted ids above, ties, zero degrees, sizes off its 16384-id chunk, degrees up to 2^32-1."""
+    ties in id order): the counting sort's classes below 1024 and the radix-sorted ids above,
+    ties, zero degrees, sizes off its 16384-id chunk, degrees up to 2^32-1."""
     import torch
     from sheep_amd import device
 
-    options(seq_sort=seq_sort)
     d = _degrees(case, np.random.default_rng(len(case)))
     seq, rank, n = device.sequence(torch.from_numpy(d.view(np.int32)).cuda().view(torch.uint32))
     torch.cuda.synchronize()
@@ -125,9 +123,6 @@ def test_sequence_from_degrees(oracle, gpu, options, seq_sort, case):
 
 
 @pytest.mark.parametrize("scale,seed,mode,env", [
-    (18, 33, 0, {"seq_sort": 1}),           # the radix-sorted sequence (the counting sort's A/B)
-    (18, 34, 1, {"seq_sort": 1}),           # the same, FILE degrees
-    (18, 35, 0, {"part_ysort": 0}),         # second partition pass gathering in stream order
     (18, 21, 0, {}),                        # partitioned gathers (m >= 2^22), overlapped pass 1
     (18, 22, 1, {}),                        # FILE degrees: self-loops count twice in pst's degree
     (16, 23, 0, {"edge_part": 1}),  # the partitioned gathers at a small size
@@ -136,7 +131,6 @@ def test_sequence_from_degrees(oracle, gpu, options, seq_sort, case):
     (16, 25, 0, {"bin_slack": -900, "edge_part": 0}),  # the same from unpartitioned records
     (17, 26, 0, {"bin_direct": 0}),         # edge pass + bin scatter (no direct binning)
     (16, 24, 0, {"edge_part": 0}),  # direct gathers, hi bins
-    (18, 25, 0, {"kb_gbits": 0}),   # the map's union-find without the giant bitmap
     (18, 26, 1, {"kb_pipe": 0}),    # one stream: rebase, map, apply in turn
     (18, 29, 0, {"bin_direct": 0}),                    # edge pass + bin scatter
     (18, 30, 0, {"part_overlap": 3}),  # fused: the degree scatter partitions the records
@@ -157,6 +151,52 @@ def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env)
     seq = oracle.degree_sequence(uv, mode)
     s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << scale, mode)
     torch.cuda.synchronize()
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_graph2tree_dev_sampled_capacities(oracle, gpu, mode):
+    """From 2^25 records the degree scatter and the first partition pass write into capacity
+    regions sized from a 1/256 sample of the records (no counting read): R-MAT 21 (2^25
+    records), seq / parent / pst bit-exact in both degree conventions, the exact pass not
+    needed."""
+    import torch
+    from sheep_amd import capi, device
+
+    uv_d = device.rmat(21, 16, 77 + mode)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << 21, mode)
+    torch.cuda.synchronize()
+    assert "degree_exact" not in dict(capi.last_timings())
+    uv = uv_d.cpu().numpy().view(np.uint32)
+    seq = oracle.degree_sequence(uv, mode)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+def test_graph2tree_dev_sampled_capacities_overflow(oracle, gpu):
+    """An input the sample misjudges: every 256th record (the sampled ones) joins ids 0 and 1,
+    the others spread over 2^20 ids, so every other degree bucket and y digit outgrows its
+    capacity.  The degrees go through the exact pass (and the partition through the hi bins'
+    fallback): still bit-exact."""
+    import torch
+    from sheep_amd import capi, device
+
+    m, n_ids = 1 << 25, 1 << 20
+    rng = np.random.default_rng(3)
+    uv = rng.integers(0, n_ids, size=(m, 2), dtype=np.uint32)
+    uv[::256] = (0, 1)
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, n_ids)
+    torch.cuda.synchronize()
+    assert "degree_exact" in dict(capi.last_timings())
+    seq = oracle.degree_sequence(uv)
     p, w = oracle.build_tree(uv, seq)
     assert n == len(seq)
     assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
@@ -404,18 +444,10 @@ def test_merge_forests_equals_whole(oracle, gpu, P):
 
 KB_KNOBS = [
     {},                                              # defaults (giant bitmap + spine)
-    {"kb_gbits": 0},                                 # the map finds every record's root
-    {"kb_defer": 0},                                 # the map resolves its misses itself
-    {"kb_defer": 0, "kb_gbits": 0, "kb_pipe": 0},
     {"kb_buckets": 4, "kb_rankb": 8},                # few, wide buckets
     {"kb_buckets": 512},                             # many buckets
     {"kb_pipe": 0},                                  # one stream, map of bucket k after apply of k-1
-    {"kb_pipe": 0, "kb_gbits": 0},
-    {"kb_refresh": 0},                               # pipelined, stale kept starts zipped as they are
     {"kb_pipe": 1, "kb_buckets": 512, "kb_rankb": 512},  # many narrow buckets
-    {"kb_pick": 0},                                  # the host's anchor (rank B0 - 1) for every map
-    {"kb_pick": 0, "kb_pipe": 0},
-    {"kb_drop": 0},                                  # in-bucket pairs of two marked ranks to the zipper
     {"kb_gsum": 0},                                  # no LDS giant summary in the map
     {"kb_gsum": 1},                                  # the summary at every size (auto: 2^27 records)
 ]
@@ -529,16 +561,14 @@ def test_degree_64k_id_buckets_repeatable(api, options):
             assert torch.equal(d, ref)
 
 
-@pytest.mark.parametrize("hist", ["1", "0"])
-def test_degree_64k_id_buckets(oracle, api, options, hist):
+def test_degree_64k_id_buckets(oracle, api, options):
     """Id spaces above 2^25 use buckets of 65536 ids: the one-read histogram with u16 LDS
-    counters in segments of <= 65535 entries (hist=1) and the two-half one (hist=0) give the
-    checker's degrees — with a hub repeated more than 65535 times in one bucket, so counts
-    cross the u16 range across segments."""
+    counters in segments of <= 65535 entries gives the checker's degrees — with a hub repeated
+    more than 65535 times in one bucket, so counts cross the u16 range across segments."""
     import torch
     from sheep_amd import capi, device
 
-    options(degb_hist=int(hist), degree=2)
+    options(degree=2)
     rng = np.random.default_rng(7)
     n_ids = (1 << 26) - 5  # above 2^26 the bucketed path does not apply (global atomics)
     m = 1 << 21

@@ -53,6 +53,23 @@ def test_multi_local_powerlaw_and_empty_shards(oracle, gpu):
     check(oracle, uv_d.cpu().numpy().view(np.uint32), 0, *out)
 
 
+def test_multi_local_hub_sequence_fallback(oracle, gpu):
+    """The sharded sequence all-gathers P histograms over degree values: with a hub whose degree
+    exceeds a rank's id slice it all-gathers the degree slices instead, same
+    sequence.  4096 ids, P = 4 (slices of 1024 ids), hub degree ~3000."""
+    import torch
+    from sheep_amd import device
+
+    rng = np.random.default_rng(7)
+    hub = np.stack([np.zeros(3000, np.uint32), rng.integers(1, 4096, 3000).astype(np.uint32)], 1)
+    rest = rng.integers(0, 4096, (20000, 2)).astype(np.uint32)
+    uv = np.ascontiguousarray(rng.permutation(np.concatenate([hub, rest])))
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    for P in (2, 4):
+        out = device.graph2tree_multi_local(shards_of(uv_d, P), 4096)
+        check(oracle, uv, 0, *out)
+
+
 def test_multi_local_known_answer(oracle, gpu):
     import json
     import os
@@ -103,9 +120,6 @@ def test_rccl_one_rank_device_and_host(oracle, gpu, hep_edges):
 @pytest.mark.parametrize("env", [{"bin_slack": -900},               # every rank's bins overflow:
                                                                     # the scatter path per rank
                                  {"bin_direct": 0},                 # edge pass + bin scatter
-                                 {"kb_pick": 0},                    # the host's anchors
-                                 {"kb_drop": 0},
-                                 {"kb_gbits": 0},                   # no giant bitmap in the maps
                                  {"kb_gsum": 1},                    # the LDS giant summary
                                  {"part_overlap": 0},               # no first pass beside the degrees
                                  {"ls_split": 0},                   # every rank runs every zipper

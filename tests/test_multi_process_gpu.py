@@ -49,6 +49,7 @@ def _rank(r, world, name, scale, seed, opts, q):
     (2, 16, 41, {}),
     (3, 17, 42, {}),                              # three ranks: uneven id slices
     (4, 16, 43, {"ls_split": 0, "ls_seq": 0}),    # replicated apply, all-reduced degrees
+    (8, 16, 44, {}),                              # the headline's P: 8 processes, 8 id slices
 ])
 def test_multi_process_host_comm(oracle, world, scale, seed, opts):
     ctx = mp.get_context("spawn")
@@ -77,3 +78,47 @@ def test_multi_process_host_comm(oracle, world, scale, seed, opts):
         assert np.array_equal(seq, oseq)
         assert np.array_equal(parent, p)
         assert np.array_equal(pst, s)
+
+
+def _seq_rank(r, world, name, shards, q):
+    try:
+        from sheep_amd import api, device
+
+        device.init(0)
+        device.comm_init_host(name, world, r)
+        try:
+            q.put((r, api.mpi_sequence(shards[r]), None))
+        finally:
+            device.comm_free()
+    except Exception as e:
+        q.put((r, None, repr(e)))
+
+
+def test_mpi_sequence_retry_on_every_rank(oracle):
+    """mpiSequence (sequence.h:65-93) where rank 0's records span only ids 0..15: its buffer
+    (max id + 1) is shorter than the global sequence, so EVERY rank gets -ERANGE with the global
+    length and every rank must retry, including rank 1, whose buffer was large enough (ADVICE
+    r03: it used to raise while rank 0 retried alone and waited forever)."""
+    rng = np.random.default_rng(5)
+    small = rng.integers(0, 16, (200, 2)).astype(np.uint32)
+    large = rng.integers(0, 5000, (20000, 2)).astype(np.uint32)
+    q = mp.get_context("spawn").Queue()
+    name = "/sheep-test-%s" % uuid.uuid4().hex[:16]
+    pc = mp.start_processes(_seq_rank, args=(2, name, [small, large], q), nprocs=2, join=False,
+                            start_method="spawn")
+    got = {}
+    try:
+        for _ in range(2):
+            r, seq, err = q.get(timeout=180)
+            assert err is None, "rank %d: %s" % (r, err)
+            got[r] = seq
+        while not pc.join(timeout=60):
+            pass
+    finally:
+        for proc in pc.processes:
+            if proc.is_alive():
+                proc.kill()
+    want = oracle.degree_sequence(np.concatenate([small, large]))
+    assert want.size > 16
+    for r in range(2):
+        assert np.array_equal(got[r], want)
