@@ -82,8 +82,8 @@ int sheep_abi_version(void);
  * kernels and never change a result.  Their defaults come from SHEEP_<NAME> environment
  * variables, read ONCE when the library first initialises a device; afterwards only these
  * calls change them (process-wide).  Names: degree, edge_part, part_overlap, kb_buckets,
- * kb_rankb, kb_pipe, tree_stats, bin_direct, bin_slack, kb_gsum, eval_pass, ls_split, ls_seq
- * (and the lab option kb_merge).
+ * kb_rankb, kb_merge, kb_pipe, tree_stats, bin_direct, bin_slack, kb_gsum, eval_pass,
+ * ls_split, ls_seq.
  * -EINVAL for an unknown name. */
 int sheep_set_option(const char* name, long long value);
 int sheep_get_option(const char* name, long long* value);

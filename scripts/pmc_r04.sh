@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 counter evidence for one RMAT-26 graph2tree step (bench.py --steps 1 --warmup 0):
 # one rocprofv3 --pmc run per counter group (MI355X_MICROARCH.md: separate passes, at most
-# 4 TCC / 8 SQ counters each), CSVs under $OUT/<pass>.  scripts/pmc_table.py turns them into
+# 4 TCC / 8 SQ counters each), CSVs under $OUT/<pass>.  scripts/pmc_r04_table.py turns them into
 # the per-kernel table (bytes, L2 hit rate, atomics, LDS conflicts, time).
 set -o pipefail
 OUT=${OUT:-gpurun_out/pmc_r04}

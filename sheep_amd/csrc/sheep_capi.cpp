@@ -370,7 +370,6 @@ struct DegInfo {
   const uint32_t* nsd = nullptr;    // rank-ordered deg - w * selfc (nullable, see sequence_dev)
   bool part_first_done = false;     // the first partition pass was launched on c.side into
                                     // e_items; c.part_ev[1] marks its end
-  bool mid_p6 = false;              // ... and wrote packed 6-byte records (launch_part_first)
   uint64_t mid_slots = 0;           // ... of which e_items holds this many (0: m)
   bool mid_caps = false;            // ... into capacity regions (launch_part_first_caps): its
                                     // overflow word is c.d_err[3]
@@ -457,6 +456,13 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   uint32_t K_e, K_r;
   kb_counts(m, &K_e, &K_r);
   uint32_t K = K_e + K_r;
+  // parent and hint interleaved (pj[2v], pj[2v + 1]): a zipper step loads one line; the parents
+  // go to d_parent after the loop
+  uint32_t* const d_out = d_parent;
+  uint32_t* pj = (uint32_t*)c.scratch.get("kb_pj", (size_t)n_seq * 8);
+  launch_pj_init(pj, n_seq, s);
+  d_parent = pj;
+  jump = pj + 1;
   uint32_t* uf = (uint32_t*)c.scratch.get("kb_uf", (size_t)n_seq * 4);
   uint32_t* label = (uint32_t*)c.scratch.get("kb_label", (size_t)n_seq * 4);
   uint32_t* linked = (uint32_t*)c.scratch.get("kb_linked", (size_t)n_seq * 4);
@@ -603,11 +609,12 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
         unsigned long long h[16];
         HIP_CHECK(hipMemcpyAsync(h, ws, 128, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
-        fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu finds %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu\n",
-                k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]);
+        fprintf(stderr, "bucket %zu ranks [%u,%u) edges %llu kept %llu inbucket_lo %llu finds %llu zip %llu steps %llu cas %llu fail %llu maxsteps %llu zroot %llu zone %llu\n",
+                k, bk[k].first, bk[k + 1].first, h[0], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]);
       }
     }
   }
+  launch_pj_parents(pj, n_seq, d_out, s);
 }
 
 // ---- hi bins (the one-pass grouping of the edge items, see sheep_kernels.hip) -------------
@@ -735,8 +742,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   if (n_seq == 0) return;
   launch_fill(d_parent, INV, n_seq, s);
   launch_fill(d_pst, 0, n_seq, s);
-  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n_seq * 4);
-  launch_fill(jump, 0, n_seq, s);
+  uint32_t* jump = nullptr;  // (the kb loop keeps its hints beside the parents)
   if (m == 0) return;
   uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
   uint64_t* items_b = (uint64_t*)c.scratch.get("e_items_b", m * 8);
@@ -780,8 +786,8 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
   if (part) {
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
       HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
-      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, di->mid_p6, pre6,
-                         di->mid_slots, di->mid_caps);
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6, di->mid_slots,
+                         di->mid_caps);
     } else {
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready,
                          pre6);
@@ -834,7 +840,6 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     if (c.h_pinned[8] || (di && di->mid_caps && c.h_pinned[10])) {
       DegInfo d2 = *di;
       d2.part_first_done = false;  // k_part's passes are run again from d_uv (unpacked)
-      d2.mid_p6 = false;
       d2.mid_caps = false;
       d2.mid_slots = 0;
       d2.yhist_ready = false;      // the first partition consumed the y-digit counts
@@ -903,8 +908,7 @@ static void merge_forests_dev(Ctx& c, const uint32_t* d_parents, uint32_t T, uin
   require_records((uint64_t)T * n, "forest merge");
   if (n == 0) return;
   launch_fill(d_parent, INV, n, s);
-  uint32_t* jump = (uint32_t*)c.scratch.get("jump", (size_t)n * 4);
-  launch_fill(jump, 0, n, s);
+  uint32_t* jump = nullptr;  // (the kb loop keeps its hints beside the parents)
   const uint64_t m = (uint64_t)T * n;
   if (m == 0) return;
   uint64_t* items = (uint64_t*)c.scratch.get("e_items", m * 8);
@@ -1035,16 +1039,15 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
                      uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr,
-                     const uint32_t* nsd = nullptr, bool mid_p6 = false,
-                     bool ids_checked = false) {
+                     const uint32_t* nsd = nullptr, bool ids_checked = false) {
   require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
   L.n_seq = n_seq;
   HIP_CHECK(hipHostMalloc(&L.h_pinned, 64, hipHostMallocDefault));
   const size_t n = std::max<uint32_t>(n_seq, 1);
-  L.parent = (uint32_t*)sc.get("ls_parent", n * 4);
-  L.jump = (uint32_t*)sc.get("ls_jump", n * 4);
+  L.parent = (uint32_t*)sc.get("ls_parent", n * 8);
+  L.jump = L.parent + 1;
   L.hcnt = (uint32_t*)sc.get("ls_hcnt", n * 4);
   L.uf = (uint32_t*)sc.get("ls_uf", n * 4);
   L.label = (uint32_t*)sc.get("ls_label", n * 4);
@@ -1066,8 +1069,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   // this rank's maps walk m records: the summary rule of tree_from_sorted
   if (knobs().kb_gsum > 0 || (knobs().kb_gsum < 0 && m >= (1ull << 27)))
     L.gsum = (uint32_t*)sc.get("ls_gsum", ((size_t)n_seq / 2048 + 2) * 4);
-  launch_fill(L.parent, INV, n, s);
-  launch_fill(L.jump, 0, n, s);
+  launch_pj_init(L.parent, (uint32_t)n, s);
   launch_fill(L.hcnt, 0, n, s);
   launch_iota(L.uf, n, s);
   launch_iota(L.label, n, s);
@@ -1115,7 +1117,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     if (part_done) {  // pass 1 ran beside the degree all-reduce and the sequence
       pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
       HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
-      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, mid_p6, pre6);
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6);
     } else {
       pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false, pre6);
@@ -1380,7 +1382,7 @@ static void ls_finish(Ctx& c, Lockstep& L, const uint32_t* d_seq, const uint32_t
     if (L.zused[z]) HIP_CHECK(hipStreamWaitEvent(s, L.zdone[z], 0));
   if (L.n_seq) {
     if (d_pst) launch_pst_from_count(d_seq, L.n_seq, d_deg, d_selfc, mode, L.hcnt, d_pst, s);
-    HIP_CHECK(hipMemcpyAsync(d_parent, L.parent, (size_t)L.n_seq * 4, hipMemcpyDeviceToDevice, s));
+    launch_pj_parents(L.parent, L.n_seq, d_parent, s);
   }
   if (!sync) return;
   HIP_CHECK(hipStreamSynchronize(s));
@@ -1519,13 +1521,11 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   const bool yh = degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s, overlap,
                              overlap ? c.part_ev[0] : nullptr);
-  // packed first-pass records (an id >= n_ids fails this call: the degree pass's ERR_RANGE)
-  const bool mid6 = overlap && knobs().bin_direct && part_p6_ok(n_ids);
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
-    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh, mid6);
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
     part_done = c.part_ev[1];
   }
@@ -1557,7 +1557,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
   ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done,
-           nsd, mid6, true);
+           nsd, true);
   if (part_done) HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));  // also when no tree is built
   check_err(c, s);
   uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);
@@ -1870,17 +1870,15 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
                             stats, s, [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
   }
   const bool overlap = !fused && ov != 0 && m > 0 && use_part(m);
-  // the first pass's records packed when the direct edge pass will read the second pass's
-  // (an id >= n_ids fails this call: the degree pass raises ERR_RANGE)
-  const bool mid6 = overlap && knobs().bin_direct && part_p6_ok(n_ids);
   // Sampled capacities (from 2^25 records, the bucketed degree path, the first pass beside
   // it): no counting read of the records — the degree scatter and the first partition pass
   // write into capacity regions sized from a 1/256 sample (launch_degree_sampled).  A region
   // that overflows sends the degrees (here, before the sequence reads them) or the partition
   // (after the edge pass, with the hi bins' overflow) through the exact pass.
-  const bool sampled = mid6 && ov == 2 && m >= (1ull << 25) && 2 * m < (1ull << 32) &&
-                       knobs().degree != 1 && degs_tmp_words(m, n_ids) > 1;
-  // packed records the mid buffer holds (capacity regions: their largest possible sum)
+  const bool sampled = overlap && knobs().bin_direct && part_p6_ok(n_ids) && ov == 2 &&
+                       m >= (1ull << 25) && 2 * m < (1ull << 32) && knobs().degree != 1 &&
+                       degs_tmp_words(m, n_ids) > 1;
+  // records the mid buffer holds (capacity regions: their largest possible sum)
   const uint64_t mid_slots = sampled ? fs_room(m, 1024) : m;
   uint32_t* ovf_deg = c.d_err + 2;
   uint32_t* ovf_part = c.d_err + 3;
@@ -1899,7 +1897,8 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   tm.mark(fused ? "degree_hist" : "degree");
   if (fused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
   if (sampled) {
-    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m * 8, mid_slots * 6));
+    // (at least m u64: the tree build takes the same buffer at that size and must not regrow it)
+    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m, mid_slots) * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench
@@ -1920,7 +1919,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     if (ov != 2) HIP_CHECK(hipEventRecord(c.part_ev[0], s));
     HIP_CHECK(hipStreamWaitEvent(c.side, c.part_ev[0], 0));
     const size_t sp = tm.span_begin("part_first", c.side);  // k_part<0>, live-timed for bench
-    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh, mid6);
+    launch_part_first(d_uv, m, n_ids, mid, pws, c.side, yh);
     tm.span_end(sp, c.side);
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
@@ -1933,7 +1932,6 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   DegInfo di;
   di.nsd = nsd;
   di.part_first_done = overlap || fused;
-  di.mid_p6 = mid6;
   di.mid_slots = mid_slots;
   di.mid_caps = sampled;
   di.ids_checked = true;

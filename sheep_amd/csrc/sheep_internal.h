@@ -52,8 +52,8 @@ struct Knobs {
                          //   space (degrees reduce-scattered; 0: all-reduced, every rank sorts all)
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
                          //   rank (0: every rank applies every bucket's zipper)
-  int kb_merge = 0;      // SHEEP_KB_MERGE (lab): merge adjacent kb buckets while together they hold
-                         //   at most kb_merge / 10000 of the records (0: off)
+  int kb_merge = 20;     // SHEEP_KB_MERGE: merge adjacent kb buckets while together they hold at
+                         //   most kb_merge / 10000 of the records (0: off)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
@@ -179,8 +179,8 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // ws: y / x digit counts, the first pass's u64 cursors, the u32 region starts of both passes'
 // outputs, the second pass's cursors, the first pass's capacity region ends (sheep_kernels.hip).
 constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024;
-// p6: the records between the passes and after them are packed to 6 bytes (sheep_kernels.hip
-// "packed 6-byte records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
+// p6: the second pass's records are packed to 6 bytes (sheep_kernels.hip "packed 6-byte
+// records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
 bool part_p6_ok(uint32_t n_rank);
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
@@ -188,14 +188,15 @@ void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, ui
 // The two passes of launch_part_gather separately (the first needs no ranks, so it can run
 // while the sequence is sorted): uv -> mid (y-digit order), then mid -> pre (x-digit order).
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
-                       uint32_t* ws, hipStream_t s, bool yhist_ready, bool p6 = false);
+                       uint32_t* ws, hipStream_t s, bool yhist_ready);
+// out6: pre is written packed; caps: mid holds launch_part_first_caps's regions (mid_slots).
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool in6 = false,
-                        bool out6 = false, uint64_t mid_slots = 0, bool caps = false);
+                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6 = false,
+                        uint64_t mid_slots = 0, bool caps = false);
 // Sampled capacities (sheep_kernels.hip, "sampled capacities"): the degree pass without a
 // counting read — a 1/256 sample sizes each bucket's and each y digit's capacity region; the
-// y regions go to part_ws for launch_part_first_caps (packed records, mid_slots of them; the
-// event caps_done marks them written).  *ovf is set when a run outgrew its region: the degrees
+// y regions go to part_ws for launch_part_first_caps (mid_slots records; the event caps_done
+// marks them written).  *ovf is set when a run outgrew its region: the degrees
 // are then invalid and the caller runs the exact pass.  False when not applicable.
 size_t degs_tmp_words(uint64_t m, uint32_t n_ids);
 // The most slots the sampled capacity regions of `items` items over n_regions can take (the
@@ -305,6 +306,11 @@ void launch_deg_of_rank(const uint32_t* S, uint32_t D, uint32_t n_seq, uint32_t*
 void launch_seq_stats64(const uint32_t* stats, uint32_t c, long long* out, hipStream_t s);
 void launch_iota(uint32_t* p, uint32_t n, hipStream_t s);
 void launch_forest_items(const uint32_t* parent, uint32_t n, uint64_t* items, hipStream_t s);
+// The kb loop's parents and hints, interleaved (pj[2v] = parent, pj[2v + 1] = hint; 2n words):
+// (INVALID, 0) for every rank; the parents out to parent[0, n).
+void launch_pj_init(uint32_t* pj, uint32_t n, hipStream_t s);
+
+void launch_pj_parents(const uint32_t* pj, uint32_t n, uint32_t* parent, hipStream_t s);
 // Partition quality (sheep_eval.hip).  ws: 4k + 8 u64: [0,3k) hash/down/up balances, [3k,4k)
 // vertex balance, then cut, self-loop records, nodes, and the distinct keys of vcom, hash,
 // down, up.  keys/keys_b: 2m u64; rtmp: rsort_tmp_words(2m) u32; deg: LLAMA degrees.

@@ -366,17 +366,15 @@ static int part_shift(uint32_t n_rank, uint32_t nd) {  // id >> shift < nd for i
 }
 
 // ---- packed 6-byte records (P6) ------------------------------------------------------------
-// Inside one digit region of a partition pass's output the digit's bits are implied, so with
-// every id below n_rank <= 2^26 a record needs 42 (first pass) or 43-45 (second pass) bits:
-//   first pass (by y digit, psh <= 16 low bits of y kept):  a = x,  b = y & (2^psh - 1);
-//   second pass (by x digit, shx <= 18 low bits of x kept): a = ry' << XH | x_lo >> 16,
-//                                                          b = x_lo & 0xFFFF,  XH = shx - 16,
+// Inside one digit region of the second partition pass's output the x digit's bits are
+// implied, so with every id below n_rank <= 2^26 a record (x, ry) needs 43-45 bits: shx <= 18
+// low bits of x and ry:  a = ry' << XH | x_lo >> 16,  b = x_lo & 0xFFFF,  XH = shx - 16, with
 // ry' = ry, or a sentinel (RY_SELF / RY_OUT / INV) folded into the top of its 32 - XH bits.
 // A buffer of m records holds the u32 array a (4m bytes) then the u16 array b (2m bytes): the
-// three passes that write or read these records move 6 bytes per record instead of 8.  A
-// reader restores the digit from the region starts (k_part_cursor) of the position's region.
-// Only for callers where an id >= n_rank fails the call anyway (graph2tree_dev, the multi-rank
-// driver: the degree pass raises ERR_RANGE): such an id loses its high bits here.
+// second pass writes and the edge pass reads 6 bytes per record instead of 8.  The edge pass
+// restores the digit from the region starts (k_part_cursor) of the position's region.  Only for
+// callers where an id >= n_rank fails the call anyway (graph2tree_dev, the multi-rank driver:
+// the degree pass raises ERR_RANGE): such an id loses its high bits here.
 struct P6Ref {
   const uint32_t* a;
   const uint16_t* b;
@@ -2304,13 +2302,14 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32
 
 // ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1), ND / NT per thread in the scan.
 // MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
-// in, m: the input and its positions.  IN6 (MODE 1): the input is the first pass's P6 output
-// (m slots): y's digit from the region starts in_starts (psh = ish), which end at
-// in_starts[PD_Y]; a position counts only below its region's fill (in_fill, capped at in_cap:
-// capacity regions leave gaps).  OUT6: the output is written as P6 records, m_out slots.
-// cap_end / ovf (nullable, MODE 0): capacity regions — a run past its digit's end is dropped
-// and *ovf set.
-template <int MODE, int NT, int IT, uint32_t ND, bool IN6 = false, bool OUT6 = false>
+// in, m: the input and its positions.  REG (MODE 1): the input lies in the first pass's
+// capacity regions (starts in_starts, which end at in_starts[PD_Y]); a position counts only
+// below its region's fill (in_fill, capped at in_cap).  OUT6 (MODE 1): the output is written
+// as packed 6-byte records, m_out of them.  cap_end / ovf (nullable, MODE 0): capacity regions —
+// a run past its digit's end keeps the part that fits and sets *ovf.
+// (Packing the first pass's records too measured no faster: 44.96 vs 44.99 ms at RMAT-26 —
+// its 16-record runs became 64- and 32-byte runs, written at 1.6x their bytes.)
+template <int MODE, int NT, int IT, uint32_t ND, bool OUT6 = false, bool REG = false>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, uint64_t m_out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
@@ -2319,18 +2318,20 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
        const unsigned long long* __restrict__ in_fill, const unsigned long long* __restrict__ in_cap,
        const unsigned long long* __restrict__ cap_end, uint32_t* ovf) {
   static_assert(ND % NT == 0 || NT % ND == 0, "digits per thread");
-  static_assert(!IN6 || MODE == 1, "packed input: the second pass only");
+  static_assert(!REG || MODE == 1, "capacity-region input: the second pass only");
+  static_assert(!OUT6 || MODE == 1, "packed output: the second pass only");
   static_assert(IT <= 32, "validity mask");
+  constexpr bool RG = REG;
   constexpr int R = ND > (uint32_t)NT ? (int)ND / NT : 1;  // digits per thread in the scan
   constexpr int PT_ITEMS = IT;
   constexpr int TILE = NT * PT_ITEMS;
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[ND], tstart[ND], hx[MODE == 0 ? PD_X : 1], wsum[NT / 64];
-  __shared__ unsigned long long gbase[ND];
-  __shared__ uint32_t sst[IN6 ? PD_Y + 2 : 1], sfill[IN6 ? PD_Y : 1], s_nv;
+  __shared__ unsigned long long gbase[ND], gcap[MODE == 0 ? ND : 1];
+  __shared__ uint32_t sst[RG ? PD_Y + 2 : 1], sfill[RG ? PD_Y : 1], s_nv;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
-  const uint64_t lim = IN6 ? min(m, (uint64_t)in_starts[PD_Y]) : m;
+  const uint64_t lim = RG ? min(m, (uint64_t)in_starts[PD_Y]) : m;
   if (tbase >= lim) return;  // (the grid covers m slots; the regions may end earlier)
   const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, lim - tbase);
   for (uint32_t i = t; i < ND; i += NT) hist[i] = 0;
@@ -2339,15 +2340,11 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
   uint32_t vm = 0;  // bit k: item k is a record
-  if (IN6) {
-    const P6Ref pin = p6_in(in, m);
-    uint32_t ya[PT_ITEMS];
-    uint16_t yb[PT_ITEMS];
+  if constexpr (REG) {
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
-      ya[k] = j < tile_n ? pin.a[tbase + j] : 0u;
-      yb[k] = j < tile_n ? pin.b[tbase + j] : (uint16_t)0;
+      rec[k] = j < tile_n ? in[tbase + j] : 0ull;
     }
     tile_regions<PD_Y>(in_starts, tbase, tile_n, sst);  // (the loads above are in flight)
     const uint32_t d0 = sst[0];
@@ -2360,9 +2357,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
       const uint64_t pos = tbase + min(j, tile_n - 1);
-      const uint32_t d = tile_digit(sst, pos);
-      rec[k] = ((uint64_t)((d << ish) | yb[k]) << 32) | ya[k];
-      vm |= (uint32_t)(j < tile_n && pos < sfill[d - d0]) << k;
+      vm |= (uint32_t)(j < tile_n && pos < sfill[tile_digit(sst, pos) - d0]) << k;
     }
   } else {
 #pragma unroll
@@ -2446,10 +2441,13 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
       const uint32_t d = t * R + r;
       tstart[d] = run;
       run += c[r];
-      unsigned long long g = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
-      if (cap_end && c[r] && g + c[r] > cap_end[d]) {  // past the digit's capacity: dropped
-        atomicOr(ovf, 1u);
-        g = ~0ull;
+      const unsigned long long g = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
+      if (MODE == 0) {
+        // capacity regions: a run past its digit's end keeps the part that fits (no unwritten
+        // hole below the region's end, which the second pass reads up to) and flags the pass
+        const unsigned long long ce = cap_end ? cap_end[d] : ~0ull;
+        if (c[r] && g + c[r] > ce) atomicOr(ovf, 1u);
+        gcap[d] = ce;
       }
       gbase[d] = g;
     }
@@ -2480,13 +2478,10 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   for (uint32_t j = t; j < n_st; j += NT) {
     uint64_t r = stage[j];
     uint32_t d = part_digit<ND>(MODE == 0 ? (uint32_t)(r >> 32) : (uint32_t)r, sh);
-    if (gbase[d] == ~0ull) continue;
     const uint64_t pos = gbase[d] + (j - tstart[d]);
+    if (MODE == 0 && pos >= gcap[d]) continue;  // past the capacity region (flagged above)
     if (!OUT6) {
       out[pos] = r;
-    } else if (MODE == 0) {  // a = x, b = y's low sh bits
-      oa[pos] = (uint32_t)r;
-      ob[pos] = (uint16_t)((uint32_t)(r >> 32) & ((1u << sh) - 1u));
     } else {  // a = ry' << xh | x_lo >> 16, b = x_lo & 0xFFFF
       // (masked: an id >= n_rank, clamped to the last digit, must not spill into ry's bits)
       const uint32_t xlo = ((uint32_t)r - (d << sh)) & ((1u << sh) - 1u);
@@ -2502,9 +2497,8 @@ bool part_p6_ok(uint32_t n_rank) {
 }
 
 // uv (x, y) -> pre (x, ry) in x-digit order, via mid (y-digit order).  ws: PART_WS_WORDS.
-// p6: mid is written packed (the second pass then reads it packed).
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
-                       uint32_t* ws, hipStream_t s, bool yhist_ready, bool p6) {
+                       uint32_t* ws, hipStream_t s, bool yhist_ready) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   uint32_t* yhist = ws;
@@ -2518,24 +2512,23 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
   }
   hipLaunchKernelGGL(k_part_cursor<PD_Y>, dim3(1), dim3(PD_Y), 0, s, yhist, cursor, ws + PW_YST);
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
-  auto k = p6 ? k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, true>
-              : k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, false>;
-  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m, mid, m,
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt), dim3(PT0_THREADS),
+                     0, s, (const uint64_t*)uv, m, mid, m,
                      cursor, xhist, sh, shx, (const uint32_t*)nullptr, n_rank, -1,
                      (const uint32_t*)nullptr, 0, (const unsigned long long*)nullptr,
                      (const unsigned long long*)nullptr, (const unsigned long long*)nullptr,
                      (uint32_t*)nullptr);
 }
 
-// The first pass into the capacity regions launch_degree_sampled left in ws (packed records,
-// mid_slots of them in mid); a run past its region's end is dropped and *ovf set.
+// The first pass into the capacity regions launch_degree_sampled left in ws (mid_slots records
+// in mid); a run past its region's end keeps what fits and sets *ovf.
 void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
                             uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   (void)hipMemsetAsync(ws + PW_X, 0, PD_X * 4, s);
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
-  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y, false, true>), dim3((unsigned)nt),
+  hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt),
                      dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m, mid, mid_slots,
                      (unsigned long long*)(ws + PW_CUR), ws + PW_X, sh, shx, (const uint32_t*)nullptr,
                      n_rank, -1, (const uint32_t*)nullptr, 0, (const unsigned long long*)nullptr,
@@ -2543,23 +2536,23 @@ void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uin
                      (const unsigned long long*)(ws + PW_YCAP), ovf);
 }
 
-// in6: mid holds the first pass's packed records (mid_slots of them: the capacity regions'
-// positions, else m; caps: capacity regions, bounded by their ends); out6: pre is written packed.
+// caps: mid holds the first pass's capacity regions (mid_slots positions); out6: pre is written
+// packed.
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
-                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool in6, bool out6,
-                        uint64_t mid_slots, bool caps) {
+                        uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6, uint64_t mid_slots,
+                        bool caps) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   const int ysh = std::max(sh - 8, 0);
   uint32_t* xhist = ws + PW_X;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
   hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
-  const uint64_t pos = in6 && mid_slots ? mid_slots : m;
+  const uint64_t pos = caps && mid_slots ? mid_slots : m;
   uint64_t nt = (pos + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
-  auto k = in6 ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
-                       : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, false>)
-               : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>
-                       : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, false>);
+  auto k = caps ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
+                        : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>)
+                : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true>
+                        : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, pos, pre, m, cursor, xhist,
                      shx, shx, rank, n_rank, ysh, (const uint32_t*)(ws + PW_YST), sh,
                      (const unsigned long long*)(ws + PW_CUR),
@@ -2570,8 +2563,8 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
                         bool yhist_ready, bool p6) {
-  launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready, p6);
-  launch_part_second(mid, m, rank, n_rank, pre, ws, s, p6, p6, m, false);
+  launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready);
+  launch_part_second(mid, m, rank, n_rank, pre, ws, s, p6, m, false);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2618,6 +2611,7 @@ constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u, ZF_LINKED = 4u;
 
 struct ZCount {
   uint32_t steps = 0, cas = 0, fail = 0;
+  uint32_t root = 0, one = 0;  // (STATS) edges starting below B0; edges done in one step
 };
 
 // One step of the insertion of pending edge (s.a, s.b); returns true when it is finished.
@@ -2631,6 +2625,7 @@ struct ZRec {  // where to record pre-bucket roots (x < B0) that a CAS links for
   uint32_t* lbuf = nullptr;
   uint32_t* lcnt = nullptr;
   uint32_t lcap = 0;
+
 };
 
 // The giant's spine inside a kb bucket [B0, B1).  G is the elimination-tree root of the
@@ -2675,10 +2670,31 @@ __device__ __forceinline__ uint32_t sp_pred(const SpineInfo& sp, uint32_t b, uin
   return INV;
 }
 
-template <int LOAD, int JUMP, bool STATS, bool REC = false, bool SPINE = false>
+// Parent and hint of rank v.  S = 1: two arrays (parent[v], jump[v]); S = 2: one interleaved
+// array, parent at pj[2v] and the hint at pj[2v + 1] (the kb loop): a step then loads both with
+// one 8-byte relaxed agent-scope load — one cache line per step, not two.  (The hint half is
+// written with plain stores and the parent half only by CAS: write-back L2s merge dirty bytes
+// only, so neither half overwrites the other.)
+template <int LOAD, int S>
+__device__ __forceinline__ void ld_pj(uint32_t* parent, uint32_t* jump, uint32_t x, uint32_t& p,
+                                      uint32_t& j) {
+  if (S == 2) {
+    const uint64_t w = __hip_atomic_load((uint64_t*)(parent + 2 * (size_t)x), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    p = (uint32_t)w;
+    j = (uint32_t)(w >> 32);
+  } else {
+    p = ld_parent<LOAD>(&parent[x]);
+    j = jump ? jump[x] : 0u;
+  }
+}
+
+template <int LOAD, int JUMP, bool STATS, bool REC = false, bool SPINE = false, int S = 1>
 __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZState& s, ZCount& c,
                                          const ZRec& rec = ZRec(),
                                          const SpineInfo& sp = SpineInfo()) {
+  static_assert(S == 1 || JUMP, "interleaved parent / hint");
+  uint32_t* const jp = S == 2 ? parent + 1 : jump;  // jp[S * v]: the hint of v
   if (STATS) c.steps++;
   if (!s.fresh) {
     // the parent, the hint and (until the walk reaches the spine) x's mark word are loaded
@@ -2686,8 +2702,8 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
     // is dropped; when the spine moves x, both are loaded again (once per pending edge).
     const bool chk = SPINE && !(s.flags & ZF_SPINE);
     const uint32_t mw = (chk && s.x >= sp.B0 && s.x < sp.B1) ? sp.bitmap[s.x >> 5] : 0u;
-    uint32_t pj = ld_parent<LOAD>(&parent[s.x]);
-    uint32_t j = JUMP ? jump[s.x] : 0u;
+    uint32_t pj, j;
+    ld_pj<LOAD, S>(parent, JUMP ? jump : nullptr, s.x, pj, j);
     if (chk && (s.x == sp.G || ((mw >> (s.x & 31)) & 1u))) {
       s.flags |= ZF_SPINE;
       if (!(s.flags & ZF_KEEP) && sp_marked(sp, s.b)) return true;
@@ -2695,13 +2711,12 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
       if (y != INV) {
         s.prev = INV;
         s.x = y;
-        pj = ld_parent<LOAD>(&parent[s.x]);
-        if (JUMP) j = jump[s.x];
+        ld_pj<LOAD, S>(parent, JUMP ? jump : nullptr, s.x, pj, j);
       }
     }
     if (JUMP) {
       if (j > s.x && j < s.b) {
-        if (s.prev != INV) jump[s.prev] = j;
+        if (s.prev != INV) jp[(size_t)S * s.prev] = j;
         s.prev = s.x;
         s.x = j;
         return false;
@@ -2715,15 +2730,15 @@ __device__ __forceinline__ bool zip_step(uint32_t* parent, uint32_t* jump, ZStat
       raise_fault(FAULT_FOREST);
       return true;
     }
-    if (JUMP && s.prev != INV) jump[s.prev] = s.p;
+    if (JUMP && s.prev != INV) jp[(size_t)S * s.prev] = s.p;
     s.prev = s.x;
     s.x = s.p;
     return false;
   }
-  if (JUMP && s.x != s.a) jump[s.a] = s.x;
+  if (JUMP && s.x != s.a) jp[(size_t)S * s.a] = s.x;
   if (s.p == s.b) return true;
   if (STATS) c.cas++;
-  uint32_t old = atomicCAS(&parent[s.x], s.p, s.b);
+  uint32_t old = atomicCAS(&parent[(size_t)S * s.x], s.p, s.b);
   if (old != s.p) {
     if (STATS) c.fail++;
     s.p = old;
@@ -2760,6 +2775,8 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, uint64_t 
   atomicAdd(&stats[2], (unsigned long long)c.cas);
   atomicAdd(&stats[3], (unsigned long long)c.fail);
   atomicMax(&stats[4], (unsigned long long)maxsteps);
+  atomicAdd(&stats[5], (unsigned long long)c.root);
+  atomicAdd(&stats[6], (unsigned long long)c.one);
 }
 
 // Lane-level work queue.  Each wave pulls chunks of edges in increasing order and
@@ -2786,7 +2803,7 @@ struct EdgeSrc {
 // Queue chunk (edges per wave refill): all waves sweep the list together, so about
 // nwaves * chunk edges are in flight — the concurrency window that the zipper's rework grows
 // with.  Set per launch by the host (qchunk).
-template <int LOAD, int JUMP, bool STATS, bool REC, bool SPINE = false>
+template <int LOAD, int JUMP, bool STATS, bool REC, bool SPINE = false, int S = 1>
 __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
                                                 uint32_t* parent, uint32_t* jump,
                                                 unsigned long long* stats,
@@ -2826,7 +2843,7 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
         if (b != INV) {
           zstart(s, a, b, fl);
           active = true;
-          if (STATS) { edges++; st0 = c.steps; }
+          if (STATS) { edges++; st0 = c.steps; c.root += a < rec.B0; }
         }
       }
       cbase += cnt < avail ? cnt : avail;
@@ -2834,10 +2851,10 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
     }
     if (__ballot(active) == 0) break;
     bool linked = false;
-    if (active && zip_step<LOAD, JUMP, STATS, REC, SPINE>(parent, jump, s, c, rec, sp)) {
+    if (active && zip_step<LOAD, JUMP, STATS, REC, SPINE, S>(parent, jump, s, c, rec, sp)) {
       active = false;
       linked = REC && (s.flags & ZF_LINKED);
-      if (STATS) maxsteps = max(maxsteps, c.steps - st0);
+      if (STATS) { maxsteps = max(maxsteps, c.steps - st0); c.one += c.steps - st0 == 1; }
     }
     if (REC) {  // the pre-bucket roots linked in this step: one append reservation per wave
       const uint64_t bal = __ballot(linked);
@@ -3356,11 +3373,13 @@ k_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* __restrict__ anc_p
 // (see k_kb_map).
 // Split lockstep (P ranks, launch_ls_apply_split): CHAIN writes only the forest part (parent,
 // spq: the bucket's zipper owner), FOLD only the union-find part (uf, gbits: every rank).
+// ps: the stride of parent[] (2: interleaved with the hints, see ld_pj).
 template <bool CHAIN, bool FOLD>
 __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uint32_t B1,
                            uint32_t* parent, uint32_t* spq, uint32_t* n_spine, uint32_t limit,
                            uint32_t* uf, uint32_t anchor, uint32_t* gbits,
-                           const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc) {
+                           const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc,
+                           uint32_t ps) {
   const uint32_t w0 = B0 >> 5, w1 = (B1 - 1) >> 5;
   const uint32_t R = FOLD ? uf_find_ro(uf, anchor_rank(anchor, anc)) : INV;
   const uint32_t X = (FOLD && gbits) ? *gx : INV;
@@ -3377,14 +3396,14 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
     while (bits) {
       uint32_t nx = (w << 5) + __ffs(bits) - 1;
       bits &= bits - 1;
-      if (CHAIN) parent[cur] = nx;
+      if (CHAIN) parent[(size_t)ps * cur] = nx;
       if (FOLD) uf[nx] = R;
       cur = nx;
     }
     if (!CHAIN) continue;
     for (uint32_t v = w + 1, k = 0; v <= w1 && k < limit; ++v, ++k) {
       uint32_t nb = word_in(bitmap, v, B0, B1);
-      if (nb) { parent[cur] = (v << 5) + __ffs(nb) - 1; break; }
+      if (nb) { parent[(size_t)ps * cur] = (v << 5) + __ffs(nb) - 1; break; }
     }
     bool has_pred = false;
     for (uint32_t v = w, k = 0; v > w0 && k < limit; --v, ++k)
@@ -3449,7 +3468,7 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
 // REC = false (split lockstep, the bucket's zipper owner): no linked roots are recorded (every
 // rank unions the pairs themselves), and G comes from *gslot, captured before the bucket's
 // union-find changed (anchor != INV means there is one).
-template <bool STATS, bool REC = true>
+template <bool STATS, bool REC = true, int S = 2>
 __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __restrict__ n_kept,
                          const uint32_t* __restrict__ bitmap, const uint32_t* __restrict__ spq,
                          const uint32_t* __restrict__ n_spine, uint32_t B0, uint32_t B1,
@@ -3458,11 +3477,13 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
                          uint32_t* n_linked, uint32_t anchor, uint32_t scan_limit,
                          uint32_t qchunk, const uint32_t* __restrict__ anc,
                          const uint32_t* __restrict__ gslot = nullptr) {
-  constexpr uint32_t LCAP = REC ? 2048 : 1;  // (512: RMAT-26 tree 16.7 -> 18.2 ms)
+  constexpr uint32_t LCAP = REC ? 2048 : 1;
   __shared__ uint32_t lbuf[LCAP];
   __shared__ uint32_t lcnt, lbase;
-  if (threadIdx.x == 0) lcnt = 0;
-  block_sync();
+  if (REC) {
+    if (threadIdx.x == 0) lcnt = 0;
+    block_sync();
+  }
   ZRec rec;
   rec.B0 = B0;
   rec.linked = linked;
@@ -3472,20 +3493,20 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
   rec.lcap = LCAP;
   EdgeSrc src{kept};
   const uint64_t nk = *n_kept;
-  if (REC) anchor = anchor_rank(anchor, anc);
+  if (!gslot) anchor = anchor_rank(anchor, anc);
   if (anchor != INV) {
     SpineInfo sp;
     sp.bitmap = bitmap;
     sp.B0 = B0;
     sp.B1 = B1;
-    sp.G = REC ? label[uf_find_ro(uf, anchor)] : *gslot;
+    sp.G = gslot ? *gslot : label[uf_find_ro(uf, anchor)];
     sp.limit = scan_limit;
     src.spq = spq;
     src.G = sp.G;
     src.np = *n_spine;
-    tree_queue_body<0, 1, STATS, REC, true>(src, src.np + nk, parent, jump, stats, rec, qchunk, sp);
+    tree_queue_body<0, 1, STATS, REC, true, S>(src, src.np + nk, parent, jump, stats, rec, qchunk, sp);
   } else {
-    tree_queue_body<0, 1, STATS, REC, false>(src, nk, parent, jump, stats, rec, qchunk);
+    tree_queue_body<0, 1, STATS, REC, false, S>(src, nk, parent, jump, stats, rec, qchunk);
   }
   if (!REC) return;
   // the block's staged linked roots: one reservation, a coalesced copy
@@ -3502,11 +3523,13 @@ __global__ void k_kb_zip(const uint64_t* __restrict__ kept, const uint32_t* __re
 // threads read the same R: no union of this launch can move it.)
 // FOLD: the giant fold ran (k_kb_spine); links between two marked ranks are skipped, and the marks are cleared
 // by k_kb_label instead (this launch reads them).
+// linked / n_linked: the pre-bucket roots the zipper linked (k_kb_zip, REC).
 template <bool FOLD>
 __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t B0,
-                           uint32_t B1, const uint32_t* __restrict__ linked,
-                           const uint32_t* __restrict__ n_linked, uint32_t* bitmap,
-                           uint32_t anchor, const uint32_t* __restrict__ anc) {
+                           uint32_t B1, uint32_t* bitmap,
+                           uint32_t anchor, const uint32_t* __restrict__ anc, uint32_t ps,
+                           const uint32_t* __restrict__ linked,
+                           const uint32_t* __restrict__ n_linked) {
   anchor = anchor_rank(anchor, anc);
   const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
@@ -3519,8 +3542,8 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
   const uint64_t total = (uint64_t)width + nl;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t v = i < width ? B0 + (uint32_t)i : linked[i - width];
-    uint32_t p = parent[v];
+    const uint32_t v = i < width ? B0 + (uint32_t)i : linked[i - width];
+    uint32_t p = parent[(size_t)ps * v];
     if (p == INV) continue;
     if (FOLD && i < width && p < B1 && ((bitmap[v >> 5] >> (v & 31)) & 1) &&
         ((bitmap[p >> 5] >> (p & 31)) & 1))
@@ -3535,11 +3558,12 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
 // reference vertex *gx gets its bit (one ballot-assembled word per 32 ranks).
 __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, uint32_t* label,
                            uint32_t B0, uint32_t B1, uint32_t* counters, uint32_t* bitmap,
-                           int clear_marks, uint32_t* gbits, const uint32_t* __restrict__ gx) {
+                           int clear_marks, uint32_t* gbits, const uint32_t* __restrict__ gx,
+                           uint32_t ps = 1) {
   const uint32_t X = gbits ? *gx : INV;
   if (X == INV) {
     for (uint32_t v = B0 + blockIdx.x * blockDim.x + threadIdx.x; v < B1; v += gridDim.x * blockDim.x)
-      if (parent[v] == INV) label[uf_find<false>(uf, v)] = v;
+      if (parent[(size_t)ps * v] == INV) label[uf_find<false>(uf, v)] = v;
   } else {
     const uint32_t RX = uf_find_ro(uf, X);
     const uint32_t v0 = B0 & ~63u;  // waves cover whole 64-rank (two-word) groups
@@ -3549,7 +3573,7 @@ __global__ void k_kb_label(const uint32_t* __restrict__ parent, uint32_t* uf, ui
       bool in = false;
       if (v >= B0) {
         const uint32_t rt = uf_find<false>(uf, v);
-        if (parent[v] == INV) label[rt] = v;
+        if (parent[(size_t)ps * v] == INV) label[rt] = v;
         in = rt == RX;
       }
       const uint64_t bal = __ballot(in);
@@ -3669,6 +3693,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
                      bool refresh, bool stats, unsigned long long* st, uint32_t* gbits,
                      const uint32_t* gx, hipStream_t s, const uint32_t* anc,
                      const uint32_t* anc_next) {
+  const uint32_t ps = 2;  // parent[2v], hint[2v + 1] (k_pj_init)
   const uint32_t scan_limit = 64;  // spine scan: bitmap words per search
   uint32_t* n_linked = counters + 1;
   uint32_t* n_spine = counters + 2;
@@ -3682,8 +3707,11 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL((k_kb_spine<true, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
-                         uf, anchor, gbits, gx, anc);
-    auto zk = stats ? k_kb_zip<true> : k_kb_zip<false>;
+                         uf, anchor, gbits, gx, anc, (uint32_t)ps);
+    // the zipper records the pre-bucket roots it links (LDS staging, one reservation per block)
+    // for k_kb_union.  (Reading them back as the kept pairs' starts instead, with no recording:
+    // tree phase +0.7 ms RMAT-26, +0.8 ms LJ-shape, +1.7 ms twitter-shape — DESIGN.md §9.)
+    auto zk = stats ? k_kb_zip<true, true, 2> : k_kb_zip<false, true, 2>;
     // zipper queue: edges per wave refill (tree phase, RMAT-26: 26.3 / 25.6 / 25.3 / 25.8 ms at
     // 64 / 256 / 512 / 1024; twitter-shape: 37.7 / 37.6 / 38.9 ms at 64 / 256 / 512; LJ-shape
     // within noise)
@@ -3701,11 +3729,11 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   unsigned ug = MAX_GRID;
   auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
   hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
-                     (const uint32_t*)linked, (const uint32_t*)n_linked, bitmap,
-                     B0 > 0 ? B0 - 1 : INV, anc_next);
+                     bitmap, B0 > 0 ? B0 - 1 : INV, anc_next, ps, (const uint32_t*)linked,
+                     (const uint32_t*)n_linked);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for((uint64_t)(B1 - B0) + 64)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold,
-                     gbits, gx);
+                     gbits, gx, ps);
 }
 
 void launch_kb_refresh(uint64_t* kept, const uint32_t* n_kept, uint32_t* uf, const uint32_t* label,
@@ -3811,7 +3839,7 @@ void launch_ls_fold_union_label(bool nonempty, uint32_t B0, uint32_t B1, uint32_
     if (anchor != INV && B1 > B0)  // the marked ranks go under the anchor's root (no forest)
       hipLaunchKernelGGL((k_kb_spine<false, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)),
                          dim3(BLOCK), 0, s, (const uint32_t*)bitmap, B0, B1, nullptr, nullptr,
-                         nullptr, 0u, uf, anchor, gbits, gx, anc);
+                         nullptr, 0u, uf, anchor, gbits, gx, anc, 1u);
     if (cap)
       hipLaunchKernelGGL(k_ls_union_pairs, dim3(MAX_GRID), dim3(BLOCK), 0, s, recv, P, ms, cap, uf,
                          anchor_next, anc_next);
@@ -3830,12 +3858,13 @@ void launch_ls_fold_union_label(bool nonempty, uint32_t B0, uint32_t B1, uint32_
 void launch_ls_zip(const uint64_t* zkept, uint32_t* zn, const uint32_t* zbm, uint32_t* zspq,
                    uint32_t B0, uint32_t B1, bool has_anchor, uint32_t* parent, uint32_t* jump,
                    hipStream_t s) {
+  const uint32_t ps = 2;
   (void)hipMemsetAsync(zn + 1, 0, 4, s);
   if (has_anchor && B1 > B0)
     hipLaunchKernelGGL((k_kb_spine<true, false>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)),
                        dim3(BLOCK), 0, s, zbm, B0, B1, parent, zspq, zn + 1, 64u, nullptr, 0u,
-                       nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
-  hipLaunchKernelGGL((k_kb_zip<false, false>), dim3(MAX_GRID), dim3(BLOCK), 0, s, zkept,
+                       nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ps);
+  hipLaunchKernelGGL((k_kb_zip<false, false, 2>), dim3(MAX_GRID), dim3(BLOCK), 0, s, zkept,
                      (const uint32_t*)zn, zbm, (const uint32_t*)zspq, (const uint32_t*)(zn + 1), B0, B1,
                      nullptr, (const uint32_t*)nullptr, parent, jump, nullptr, nullptr, nullptr,
                      has_anchor ? 0u : INV, 64u, 256u, (const uint32_t*)nullptr,
@@ -4026,6 +4055,23 @@ void launch_ls_unpack(const uint64_t* recv, uint32_t P, uint32_t ms, uint32_t ca
 
 // Items of one forest over n ranks for a union build: (parent[v] << 32 | v); a root's INVALID
 // parent becomes an INVALID hi, which sorts after every rank.
+// The kb loop's interleaved parent / hint words: (INVALID, 0) to start; the parents out.
+__global__ void k_pj_init(uint64_t* pj, uint32_t n) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x)
+    pj[v] = (uint64_t)INV;
+}
+__global__ void k_pj_parents(const uint64_t* __restrict__ pj, uint32_t n, uint32_t* parent) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x)
+    parent[v] = (uint32_t)pj[v];
+}
+void launch_pj_init(uint32_t* pj, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_pj_init, dim3(grid_for(n)), dim3(BLOCK), 0, s, (uint64_t*)pj, n);
+}
+void launch_pj_parents(const uint32_t* pj, uint32_t n, uint32_t* parent, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_pj_parents, dim3(grid_for(n)), dim3(BLOCK), 0, s, (const uint64_t*)pj, n,
+                            parent);
+}
+
 __global__ void k_forest_items(const uint32_t* __restrict__ parent, uint32_t n,
                                uint64_t* __restrict__ items) {
   for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x)
