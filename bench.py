@@ -222,7 +222,7 @@ def main():
         # Roofline of the dominant kernel: the one with the most time per step among the
         # kernels bracketed live by HIP events on the stream they run on.
         # "algo" is SURVEY §8(d)'s compulsory bytes attributed to the kernel: the degree pass's
-        # one read of the records (k_fh_count), the degree writes (the histogram), the rank/tree
+        # one read of the records (k_front_fused / k_fh_count), the degree writes (the histogram), the rank/tree
         # pass's one read of the records plus the hi counts (k_kb_map); regrouping passes and
         # rank gathers count zero there.  "io" is the kernel's own streaming bytes (reads of its
         # input, writes of its output, 4 B per gathered rank), reported beside it.
@@ -234,6 +234,7 @@ def main():
                  ("k_edge_bin", "edge_pass", None, 0, 20 * recs),
                  ("k_part<1>", "partition", None, 0, 20 * recs),
                  ("k_part<0>", "part_first", "part_first#", 0, 16 * recs),
+                 ("k_front_fused", "front_fused", None, 8 * recs, 16 * recs),
                  ("k_fh_scatter", "degree_scatter", None, 0, 20 * recs),
                  ("k_fh_count", "degree_count", None, 8 * recs, 8 * recs),
                  ("k_degb_hist16", "degree_hist", None, 4 * n_ids, 4 * recs + 4 * n_ids)]

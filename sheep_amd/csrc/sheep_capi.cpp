@@ -373,6 +373,7 @@ struct DegInfo {
   uint64_t mid_slots = 0;           // ... of which e_items holds this many (0: m)
   bool mid_caps = false;            // ... into capacity regions (launch_part_first_caps): its
                                     // overflow word is c.d_err[3]
+  bool mid_p6 = false;              // ... packed by the fused front pass (launch_front_fused)
   bool ids_checked = false;         // an id >= n_rank fails the call anyway (the degree pass's
                                     // ERR_RANGE): the partition passes may pack (part_p6_ok)
 };
@@ -787,7 +788,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
       HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
       launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6, di->mid_slots,
-                         di->mid_caps);
+                         di->mid_caps, di->mid_p6);
     } else {
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready,
                          pre6);
@@ -841,6 +842,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
       DegInfo d2 = *di;
       d2.part_first_done = false;  // k_part's passes are run again from d_uv (unpacked)
       d2.mid_caps = false;
+      d2.mid_p6 = false;
       d2.mid_slots = 0;
       d2.yhist_ready = false;      // the first partition consumed the y-digit counts
       build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, tm, &d2, false);
@@ -1853,7 +1855,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   // the degree pass's first kernel: it runs on the side stream beside the rest of the degree
   // pass and the sequence sort (SHEEP_PART_OVERLAP=0: in line, after them; =1: after the
   // whole degree pass).
-  const int ov = knobs().part_overlap;
+  int ov = knobs().part_overlap;
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
   // Fused (ov 3, and always past 2^31 records, where the endpoint offsets of the unfused
   // degree pass end): the degree pass itself writes the records grouped by y bucket
@@ -1869,6 +1871,13 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     fused = launch_fh_front(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, mid, pws,
                             stats, s, [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
   }
+  // Fused sampled (ov 4): ONE read of the records for the degrees and the first partition pass
+  // (launch_front_fused; packed first-pass records in sampled capacity regions).
+  const bool ffused = !fused && ov == 4 && use_part(m) && knobs().bin_direct &&
+                      part_p6_ok(n_ids) && m >= (1ull << 25) && knobs().degree != 1 &&
+                      front_fused_ok(m, n_ids) && degs_tmp_words(m, n_ids) > 1;
+  if (ffused) fused = true;
+  if (ov == 4 && !ffused) ov = 2;  // (below 2^25 records, or ids it cannot take: beside)
   const bool overlap = !fused && ov != 0 && m > 0 && use_part(m);
   // Sampled capacities (from 2^25 records, the bucketed degree path, the first pass beside
   // it): no counting read of the records — the degree scatter and the first partition pass
@@ -1879,12 +1888,29 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
                        m >= (1ull << 25) && 2 * m < (1ull << 32) && knobs().degree != 1 &&
                        degs_tmp_words(m, n_ids) > 1;
   // records the mid buffer holds (capacity regions: their largest possible sum)
-  const uint64_t mid_slots = sampled ? fs_room(m, 1024) : m;
+  const uint64_t mid_slots = (sampled || ffused) ? (fs_room(m, 1024) + 7) & ~7ull : m;
   uint32_t* ovf_deg = c.d_err + 2;
   uint32_t* ovf_part = c.d_err + 3;
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   bool yh = false;
-  if (sampled) {
+  if (ffused) {
+    HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words
+    uint32_t* tmp = (uint32_t*)c.scratch.get("degs_tmp", degs_tmp_words(m, n_ids) * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
+    uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m, mid_slots) * 8);
+    launch_front_fused(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, pws, mid, mid_slots,
+                       stats, ovf_deg, ovf_part, s,
+                       [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
+    tm.mark("degree_hist");
+    HIP_CHECK(hipEventRecord(c.part_ev[1], s));
+    // the degrees are complete unless an x bucket outgrew its region
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c.h_pinned[4]) {
+      degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, false, nullptr, stats);
+      tm.mark("degree_exact");
+    }
+  } else if (sampled) {
     HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words
     uint32_t* tmp = (uint32_t*)c.scratch.get("degs_tmp", degs_tmp_words(m, n_ids) * 4);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
@@ -1894,8 +1920,8 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     yh = degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, true,
                     overlap && ov == 2 ? c.part_ev[0] : nullptr, stats);
   }
-  tm.mark(fused ? "degree_hist" : "degree");
-  if (fused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
+  if (!ffused) tm.mark(fused ? "degree_hist" : "degree");
+  if (fused && !ffused) HIP_CHECK(hipEventRecord(c.part_ev[1], s));
   if (sampled) {
     // (at least m u64: the tree build takes the same buffer at that size and must not regrow it)
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m, mid_slots) * 8);
@@ -1933,7 +1959,8 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   di.nsd = nsd;
   di.part_first_done = overlap || fused;
   di.mid_slots = mid_slots;
-  di.mid_caps = sampled;
+  di.mid_caps = sampled || ffused;
+  di.mid_p6 = ffused;
   di.ids_checked = true;
   di.yhist_ready = yh;
   di.seq = d_seq;

@@ -37,9 +37,11 @@ struct Scratch {
 struct Knobs {
   int degree = 0;        // SHEEP_DEGREE: 0 auto (bucketed from 2^18 records), 1 atomic, 2 bucketed
   int edge_part = -1;    // SHEEP_EDGE_PART: partitioned rank gathers; -1 auto (m >= 2^22), 0, 1
-  int part_overlap = 2;  // SHEEP_PART_OVERLAP: first partition pass beside the degree pass (2),
-                         //   after it (1), in line (0), fused into the degree scatter (3,
-                         //   graph2tree_dev; taken anyway from 2^31 records)
+  int part_overlap = 4;  // SHEEP_PART_OVERLAP: one read for the degrees and the first partition
+                         //   pass into sampled regions (4, graph2tree_dev from 2^25 records;
+                         //   else 2), the first pass beside the degree pass (2), after it (1),
+                         //   in line (0), fused into a counted degree scatter (3; taken anyway
+                         //   from 2^31 records)
   int kb_buckets = 0;    // SHEEP_KB_BUCKETS: kb buckets cut at edge quantiles (0 = auto)
   int kb_rankb = 0;      // SHEEP_KB_RANKB: kb buckets cut at rank quantiles (0 = auto)
   int kb_pipe = 1;       // SHEEP_KB_PIPE: map of bucket k+1 beside the apply of bucket k
@@ -189,10 +191,11 @@ void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, ui
 // while the sequence is sorted): uv -> mid (y-digit order), then mid -> pre (x-digit order).
 void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
                        uint32_t* ws, hipStream_t s, bool yhist_ready);
-// out6: pre is written packed; caps: mid holds launch_part_first_caps's regions (mid_slots).
+// out6: pre is written packed; caps: mid holds launch_part_first_caps's regions (mid_slots);
+// in6 (with caps): ... launch_front_fused's packed ones.
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6 = false,
-                        uint64_t mid_slots = 0, bool caps = false);
+                        uint64_t mid_slots = 0, bool caps = false, bool in6 = false);
 // Sampled capacities (sheep_kernels.hip, "sampled capacities"): the degree pass without a
 // counting read — a 1/256 sample sizes each bucket's and each y digit's capacity region; the
 // y regions go to part_ws for launch_part_first_caps (mid_slots records; the event caps_done
@@ -206,6 +209,16 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
                            uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                            uint32_t* part_ws, uint64_t mid_slots, uint32_t* stats, uint32_t* ovf,
                            hipStream_t s, hipEvent_t caps_done);
+// The fused front pass (sheep_kernels.hip k_front_fused): degrees and the first partition from
+// ONE read of the records, into sampled capacity regions (mid_slots, a multiple of 8, packed
+// records in mid).  *ovf_x: the degrees need the exact pass; *ovf_y: the partition must be
+// redone from uv.  False when not applicable (front_fused_ok).
+bool front_fused_ok(uint64_t m, uint32_t n_ids);
+bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+                        uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
+                        uint32_t* part_ws, uint64_t* mid, uint64_t mid_slots, uint32_t* stats,
+                        uint32_t* ovf_x, uint32_t* ovf_y, hipStream_t s,
+                        void (*mark)(void*, const char*) = nullptr, void* mark_arg = nullptr);
 void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
                             uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,

@@ -541,7 +541,8 @@ static constexpr uint32_t FS_STRIDE = 256;
 
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_front_sample(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
-               uint32_t NB, int psh, uint32_t* __restrict__ scnt /* NB, then PD_Y */) {
+               uint32_t NB, int psh, uint32_t* __restrict__ scnt /* NB, then PD_Y */,
+               int xonly /* the fused pass: x endpoints only in the buckets */) {
   __shared__ uint32_t hb[DEGB_NB], hy[PD_Y];
   for (uint32_t i = threadIdx.x; i < DEGB_NB; i += DEGB_THREADS) { hb[i] = 0; hy[i] = 0; }
   block_sync();
@@ -550,8 +551,8 @@ k_front_sample(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
        k += (uint64_t)gridDim.x * DEGB_THREADS) {
     const uint2 e = uv[k * FS_STRIDE];
     if (e.x >= n_ids || e.y >= n_ids) continue;  // the scatter reports it
-    atomicAdd(&hb[e.x >> SH], 1u);
-    if (file_mode || e.x != e.y) atomicAdd(&hb[e.y >> SH], 1u);
+    if (!xonly) atomicAdd(&hb[e.x >> SH], 1u);
+    if (file_mode || e.x != e.y) atomicAdd(&hb[(xonly ? e.x : e.y) >> SH], 1u);
     atomicAdd(&hy[part_digit<PD_Y>(e.y, psh)], 1u);
   }
   block_sync();
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(1024)
 k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_t ep_slots,
              uint64_t mid_slots, unsigned long long* bst, unsigned long long* bcur,
              unsigned long long* bcap, uint32_t* ystart, unsigned long long* ycur,
-             unsigned long long* ycap) {
+             unsigned long long* ycap, unsigned long long* ys64 /* nullable: ystart as u64 */) {
   __shared__ unsigned long long ws[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int pass = 0; pass < 2; ++pass) {
@@ -605,6 +606,7 @@ k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_
     if ((uint32_t)t < n) {
       if (pass) {
         ystart[t] = (uint32_t)st;
+        if (ys64) ys64[t] = st;
         ycur[t] = st;
         ycap[t] = end;
       } else {
@@ -614,7 +616,10 @@ k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_
       }
     }
     if (t == 0) {
-      if (pass) ystart[n] = (uint32_t)(fits ? total : 0ull);
+      if (pass) {
+        ystart[n] = (uint32_t)(fits ? total : 0ull);
+        if (ys64) ys64[n] = fits ? total : 0ull;
+      }
       else bst[n] = fits ? total : 0ull;
     }
     block_sync();
@@ -693,6 +698,129 @@ k_degb_scatter_cap(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int
   }
 }
 
+// The fused front pass (graph2tree_dev, part_overlap 4): ONE read of the records does the
+// degree scatter's x half and the first partition pass, into the sampled capacity regions of
+// k_front_caps:
+//   the records go out grouped by y digit, packed (P6F): x as a u32 array oa, y's low bits
+//     (y - digit << SH, < 2^16) as a u16 array ob, both indexed by the record's position;
+//   the x endpoints (LLAMA: x != y only, a self-loop counts once) go out as u16 by x bucket.
+// The histogram then counts y from ob and x from ep (SH == the y-digit shift: the buckets ARE
+// the y digits), and k_part<1> reads (oa, ob) and restores y's digit from the region starts.
+// Bytes per record: 8 read + 4 + 2 (records) + 2 (x endpoint) written, against 8 + 4 (degree
+// scatter) and 8 + 8 (first pass) before; the histogram reads the same 4.
+// Tile: FF_NT x FF_IT records.  LDS: the tile staged twice 64 KB (x; digit << 16 | y_lo), the x
+// endpoints restaged into the first half, and the run tables of both sorts.
+static constexpr int FF_NT = 1024, FF_IT = 16;
+__global__ void __launch_bounds__(FF_NT)
+k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
+              uint32_t NB, uint32_t* __restrict__ oa, uint16_t* __restrict__ ob,
+              unsigned long long* ycur, const unsigned long long* __restrict__ ycap,
+              unsigned long long* bcur, const unsigned long long* __restrict__ bcap,
+              uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc, uint32_t* ovf_y,
+              uint32_t* ovf_x, uint32_t* err, uint32_t* __restrict__ xhist, int shx) {
+  constexpr int TILE = FF_NT * FF_IT;
+  __shared__ uint32_t sa[TILE], sb[TILE];
+  __shared__ uint32_t ty[DEGB_NB + 1], tx[DEGB_NB + 1], hxd[PD_X], wsum[2 * (FF_NT / 64)];
+  __shared__ unsigned long long gy[DEGB_NB], gx[DEGB_NB];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t lmask = (1u << SH) - 1u;
+  for (uint32_t i = t; i < DEGB_NB; i += FF_NT) { ty[i] = 0; tx[i] = 0; }
+  for (uint32_t i = t; i < PD_X; i += FF_NT) hxd[i] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint32_t cn = (uint32_t)min((uint64_t)TILE, m - base);
+  uint2 e[FF_IT];
+#pragma unroll
+  for (int k = 0; k < FF_IT; ++k) {
+    const uint32_t i = (uint32_t)k * FF_NT + t;
+    e[k] = i < cn ? ld_rec_nt(uv + base + i) : make_uint2(INV, INV);
+  }
+  block_sync();
+  uint32_t ly[FF_IT], lx[FF_IT];  // rank within the tile's y run / x run (INV: none)
+#pragma unroll
+  for (int k = 0; k < FF_IT; ++k) {
+    ly[k] = INV;
+    lx[k] = INV;
+    const uint2 r = e[k];
+    if (r.x >= n_ids || r.y >= n_ids) {
+      if ((uint32_t)k * FF_NT + t < cn) atomicOr(err, ERR_RANGE);
+      continue;
+    }
+    ly[k] = atomicAdd(&ty[r.y >> SH], 1u);
+    const bool loop = r.x == r.y;
+    if (file_mode || !loop) lx[k] = atomicAdd(&tx[r.x >> SH], 1u);
+    if (loop && selfc) atomicAdd(&selfc[r.x], 1u);
+    atomicAdd(&hxd[part_digit<PD_X>(r.x, shx)], 1u);
+  }
+  block_sync();
+  // both run tables: exclusive starts in the tile, and the global runs (capacity regions: a y
+  // run keeps the part that fits; an x run that does not fit is dropped — either sets its flag)
+  {
+    const uint32_t c1 = (uint32_t)t < NB ? ty[t] : 0u, c2 = (uint32_t)t < NB ? tx[t] : 0u;
+    const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2);
+    if (lane == 63) { wsum[w] = i1; wsum[FF_NT / 64 + w] = i2; }
+    unsigned long long g1 = 0, g2 = ~0ull;
+    if ((uint32_t)t < NB) {
+      if (c1) {
+        g1 = atomicAdd(&ycur[t], (unsigned long long)c1);
+        if (g1 + c1 > ycap[t]) atomicOr(ovf_y, 1u);
+      }
+      if (c2) {
+        g2 = atomicAdd(&bcur[t], (unsigned long long)c2);
+        if (g2 + c2 > bcap[t]) {
+          atomicOr(ovf_x, 1u);
+          g2 = ~0ull;
+        }
+      }
+      gy[t] = g1;
+      gx[t] = g2;
+    }
+    block_sync();
+    uint32_t a1 = 0, a2 = 0;
+    for (int i = 0; i < w; ++i) { a1 += wsum[i]; a2 += wsum[FF_NT / 64 + i]; }
+    if ((uint32_t)t < NB) { ty[t] = a1 + i1 - c1; tx[t] = a2 + i2 - c2; }
+    if (t == FF_NT - 1) {
+      uint32_t s1 = 0, s2 = 0;
+      for (int i = 0; i < FF_NT / 64; ++i) { s1 += wsum[i]; s2 += wsum[FF_NT / 64 + i]; }
+      ty[NB] = s1;
+      tx[NB] = s2;
+    }
+  }
+  for (uint32_t i = t; i < PD_X; i += FF_NT)
+    if (hxd[i]) atomicAdd(&xhist[i], hxd[i]);
+  block_sync();
+#pragma unroll
+  for (int k = 0; k < FF_IT; ++k)
+    if (ly[k] != INV) {
+      const uint32_t d = e[k].y >> SH, j = ty[d] + ly[k];
+      sa[j] = e[k].x;
+      sb[j] = (d << 16) | (e[k].y & lmask);
+    }
+  block_sync();
+  const uint32_t ny = ty[NB];
+  for (uint32_t j = t; j < ny; j += FF_NT) {  // flat: every lane busy
+    const uint32_t v = sb[j], d = v >> 16;
+    const unsigned long long pos = gy[d] + (j - ty[d]);
+    if (pos < ycap[d]) {
+      oa[pos] = sa[j];
+      ob[pos] = (uint16_t)(v & 0xFFFFu);
+    }
+  }
+  block_sync();
+#pragma unroll
+  for (int k = 0; k < FF_IT; ++k)
+    if (lx[k] != INV) {
+      const uint32_t b = e[k].x >> SH;
+      sa[tx[b] + lx[k]] = (b << 16) | (e[k].x & lmask);
+    }
+  block_sync();
+  const uint32_t nx = tx[NB];
+  for (uint32_t j = t; j < nx; j += FF_NT) {
+    const uint32_t v = sa[j], b = v >> 16;
+    const unsigned long long g = gx[b];
+    if (g != ~0ull) ep[g + (j - tx[b])] = (uint16_t)(v & 0xFFFFu);
+  }
+}
+
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
@@ -700,7 +828,8 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
             uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
             const unsigned long long* __restrict__ bstart2 = nullptr,
             const uint64_t* __restrict__ rec0 = nullptr,
-            const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */) {
+            const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */,
+            const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */) {
   __shared__ uint32_t cnt[DEGB_HALF];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
@@ -718,6 +847,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
   if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[b]);  // (a region's fill past its end: dropped)
+  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[b]);
   if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
     const uint32_t lm = (1u << SH) - 1u;
     for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
@@ -800,7 +930,8 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
               uint32_t* __restrict__ stats, int plain, const uint16_t* __restrict__ ep2 = nullptr,
               const unsigned long long* __restrict__ bstart2 = nullptr,
               const uint64_t* __restrict__ rec0 = nullptr,
-              const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */) {
+              const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */,
+              const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */) {
   __shared__ uint32_t pk[32768];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -818,6 +949,7 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
   if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[b]);
+  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[b]);
   for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
     const uint64_t g1 = min(g0 + 65535, s1);
     for (uint32_t i = threadIdx.x; i < 32768; i += DEGB_THREADS) pk[i] = 0;
@@ -994,7 +1126,8 @@ size_t degs_tmp_words(uint64_t m, uint32_t n_ids) {
   uint32_t NB = 0;
   if (!degb_params(n_ids, &SH, &NB)) return 1;
   // samples (2 x 1024), bucket starts / cursors / ends (u64), the u16 entries (+16-B pad)
-  return 2 * DEGB_NB + 2 * (3 * (size_t)DEGB_NB + 2) + (degs_ep_slots(m, NB) + 1) / 2 + 16;
+  // (+ the fused pass's u64 y starts: its x-only entries need half the room)
+  return 2 * DEGB_NB + 2 * (4 * (size_t)DEGB_NB + 3) + (degs_ep_slots(m, NB) + 1) / 2 + 16;
 }
 
 bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
@@ -1016,10 +1149,11 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
   const unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
   hipLaunchKernelGGL(k_front_sample, dim3(sg), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m, n_ids,
-                     file_mode, SH, NB, psh, scnt);
+                     file_mode, SH, NB, psh, scnt, 0);
   hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
                      degs_ep_slots(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST,
-                     (unsigned long long*)(part_ws + PW_CUR), (unsigned long long*)(part_ws + PW_YCAP));
+                     (unsigned long long*)(part_ws + PW_CUR), (unsigned long long*)(part_ws + PW_YCAP),
+                     (unsigned long long*)nullptr);
   if (caps_done) (void)hipEventRecord(caps_done, s);
   const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   hipLaunchKernelGGL(k_degb_scatter_cap, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
@@ -1036,6 +1170,71 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)nullptr, (const unsigned long long*)nullptr,
                        (const uint64_t*)nullptr, (const unsigned long long*)bcur);
+  return true;
+}
+
+// The fused front pass (k_front_fused) and its histogram: degrees (deg, selfc), the first
+// partition's packed records in mid (mid_slots positions: u32 x array, then u16 y_lo array) and
+// its region tables in part_ws (PW_YST / PW_CUR / PW_YCAP, the x digits at PW_X).  tmp:
+// degs_tmp_words.  ovf_x: an x bucket outgrew its region (the degrees are then incomplete: the
+// caller runs the exact pass); ovf_y: a y region (the caller partitions again from uv).
+bool front_fused_ok(uint64_t m, uint32_t n_ids) {
+  int SH;
+  uint32_t NB;
+  return m > 0 && n_ids > 0 && degb_params(n_ids, &SH, &NB) && 2 * m < (1ull << 32) &&
+         part_shift(n_ids, PD_Y) == SH && SH <= 16 && NB <= DEGB_NB;
+}
+
+bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
+                        uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
+                        uint32_t* part_ws, uint64_t* mid, uint64_t mid_slots, uint32_t* stats,
+                        uint32_t* ovf_x, uint32_t* ovf_y, hipStream_t s,
+                        void (*mark)(void*, const char*), void* mark_arg) {
+  int SH;
+  uint32_t NB;
+  if (!front_fused_ok(m, n_ids) || mid_slots % 8 != 0) return false;
+  degb_params(n_ids, &SH, &NB);
+  uint32_t* scnt = tmp;
+  unsigned long long* bst = (unsigned long long*)(tmp + 2 * DEGB_NB);
+  unsigned long long* bcur = bst + DEGB_NB + 1;
+  unsigned long long* bcap = bcur + DEGB_NB;
+  unsigned long long* ys64 = bcap + DEGB_NB + 1;
+  uint16_t* ep = (uint16_t*)(((uintptr_t)(ys64 + DEGB_NB + 1) + 15) & ~(uintptr_t)15);
+  if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  (void)hipMemsetAsync(scnt, 0, 2 * DEGB_NB * 4, s);
+  (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
+  const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
+  const unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
+  hipLaunchKernelGGL(k_front_sample, dim3(sg), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m, n_ids,
+                     file_mode, SH, NB, SH, scnt, 1);
+  unsigned long long* ycur = (unsigned long long*)(part_ws + PW_CUR);
+  unsigned long long* ycap = (unsigned long long*)(part_ws + PW_YCAP);
+  hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
+                     fs_room(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST, ycur, ycap, ys64);
+  if (mark) mark(mark_arg, "degree_sample");
+  uint32_t* oa = (uint32_t*)mid;
+  uint16_t* ob = (uint16_t*)(oa + mid_slots);
+  const unsigned nt = (unsigned)((m + FF_NT * FF_IT - 1) / (FF_NT * FF_IT));
+  hipLaunchKernelGGL(k_front_fused, dim3(nt), dim3(FF_NT), 0, s, (const uint2*)uv, m, n_ids,
+                     file_mode, SH, NB, oa, ob, ycur, (const unsigned long long*)ycap, bcur,
+                     (const unsigned long long*)bcap, ep, selfc, ovf_y, ovf_x, err,
+                     part_ws + PW_X, part_shift(n_ids, PD_X));
+  if (mark) mark(mark_arg, "front_fused");
+  // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
+  if (SH > 15)
+    hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, NB, n_ids, deg,
+                       (const unsigned long long*)bst, stats, DEGB_PLAIN16, (const uint16_t*)ob,
+                       (const unsigned long long*)ys64, (const uint64_t*)nullptr,
+                       (const unsigned long long*)bcur, (const unsigned long long*)ycur);
+  else
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, NB, SH, 1u, n_ids,
+                       deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
+                       (const uint16_t*)ob, (const unsigned long long*)ys64,
+                       (const uint64_t*)nullptr, (const unsigned long long*)bcur,
+                       (const unsigned long long*)ycur);
   return true;
 }
 
@@ -2309,7 +2508,8 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32
 // a run past its digit's end keeps the part that fits and sets *ovf.
 // (Packing the first pass's records too measured no faster: 44.96 vs 44.99 ms at RMAT-26 —
 // its 16-record runs became 64- and 32-byte runs, written at 1.6x their bytes.)
-template <int MODE, int NT, int IT, uint32_t ND, bool OUT6 = false, bool REG = false>
+template <int MODE, int NT, int IT, uint32_t ND, bool OUT6 = false, bool REG = false,
+          bool IN6 = false>
 __global__ void __launch_bounds__(NT)
 k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, uint64_t m_out,
        unsigned long long* __restrict__ cursor, uint32_t* __restrict__ xhist, int sh, int shx,
@@ -2321,6 +2521,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   static_assert(!REG || MODE == 1, "capacity-region input: the second pass only");
   static_assert(!OUT6 || MODE == 1, "packed output: the second pass only");
   static_assert(IT <= 32, "validity mask");
+  static_assert(!IN6 || REG, "packed input: the fused pass's capacity regions");
   constexpr bool RG = REG;
   constexpr int R = ND > (uint32_t)NT ? (int)ND / NT : 1;  // digits per thread in the scan
   constexpr int PT_ITEMS = IT;
@@ -2341,10 +2542,20 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   uint32_t li[PT_ITEMS];
   uint32_t vm = 0;  // bit k: item k is a record
   if constexpr (REG) {
+    // IN6: the fused front pass's packed records (k_front_fused): x from the u32 array, y's low
+    // bits from the u16 array after it (m positions each), y's digit from the region
+    const uint32_t* ia = (const uint32_t*)in;
+    const uint16_t* ib = (const uint16_t*)(ia + m);
+    uint16_t yb[IN6 ? PT_ITEMS : 1];
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
-      rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+      if (IN6) {
+        rec[k] = j < tile_n ? ia[tbase + j] : 0u;
+        yb[k] = j < tile_n ? ib[tbase + j] : (uint16_t)0;
+      } else {
+        rec[k] = j < tile_n ? in[tbase + j] : 0ull;
+      }
     }
     tile_regions<PD_Y>(in_starts, tbase, tile_n, sst);  // (the loads above are in flight)
     const uint32_t d0 = sst[0];
@@ -2357,7 +2568,9 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
       const uint64_t pos = tbase + min(j, tile_n - 1);
-      vm |= (uint32_t)(j < tile_n && pos < sfill[tile_digit(sst, pos) - d0]) << k;
+      const uint32_t d = tile_digit(sst, pos);
+      vm |= (uint32_t)(j < tile_n && pos < sfill[d - d0]) << k;
+      if (IN6) rec[k] |= (uint64_t)((d << ish) | yb[k]) << 32;
     }
   } else {
 #pragma unroll
@@ -2540,7 +2753,7 @@ void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uin
 // packed.
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6, uint64_t mid_slots,
-                        bool caps) {
+                        bool caps, bool in6) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   const int ysh = std::max(sh - 8, 0);
@@ -2549,8 +2762,10 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
   const uint64_t pos = caps && mid_slots ? mid_slots : m;
   uint64_t nt = (pos + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
-  auto k = caps ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
-                        : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>)
+  auto k = caps ? (in6 ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true, true>
+                               : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true, true>)
+                       : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
+                               : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>))
                 : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true>
                         : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, pos, pre, m, cursor, xhist,
@@ -2564,7 +2779,7 @@ void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, ui
                         uint64_t* mid, uint64_t* pre, uint32_t* ws, hipStream_t s,
                         bool yhist_ready, bool p6) {
   launch_part_first(uv, m, n_rank, mid, ws, s, yhist_ready);
-  launch_part_second(mid, m, rank, n_rank, pre, ws, s, p6, m, false);
+  launch_part_second(mid, m, rank, n_rank, pre, ws, s, p6, m, false, false);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -158,19 +158,23 @@ def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env)
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_graph2tree_dev_sampled_capacities(oracle, gpu, mode):
-    """From 2^25 records the degree scatter and the first partition pass write into capacity
-    regions sized from a 1/256 sample of the records (no counting read): R-MAT 21 (2^25
-    records), seq / parent / pst bit-exact in both degree conventions, the exact pass not
-    needed."""
+@pytest.mark.parametrize("mode,ov", [(0, 4), (1, 4), (0, 2), (1, 2)])
+def test_graph2tree_dev_sampled_capacities(oracle, gpu, options, mode, ov):
+    """From 2^25 records the front half writes into capacity regions sized from a 1/256 sample
+    of the records (no counting read): one fused read for the degrees and the packed first
+    partition (part_overlap 4, k_front_fused), or the degree scatter beside the first
+    partition pass (2).  R-MAT 21 (2^25 records), seq / parent / pst bit-exact in both degree
+    conventions, the exact pass not needed."""
     import torch
     from sheep_amd import capi, device
 
+    options(part_overlap=ov)
     uv_d = device.rmat(21, 16, 77 + mode)
     s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << 21, mode)
     torch.cuda.synchronize()
-    assert "degree_exact" not in dict(capi.last_timings())
+    t = dict(capi.last_timings())
+    assert "degree_exact" not in t
+    assert ("front_fused" in t) == (ov == 4)
     uv = uv_d.cpu().numpy().view(np.uint32)
     seq = oracle.degree_sequence(uv, mode)
     p, w = oracle.build_tree(uv, seq)
@@ -180,14 +184,16 @@ def test_graph2tree_dev_sampled_capacities(oracle, gpu, mode):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
-def test_graph2tree_dev_sampled_capacities_overflow(oracle, gpu):
+@pytest.mark.parametrize("ov", [4, 2])
+def test_graph2tree_dev_sampled_capacities_overflow(oracle, gpu, options, ov):
     """An input the sample misjudges: every 256th record (the sampled ones) joins ids 0 and 1,
     the others spread over 2^20 ids, so every other degree bucket and y digit outgrows its
     capacity.  The degrees go through the exact pass (and the partition through the hi bins'
-    fallback): still bit-exact."""
+    fallback): still bit-exact, fused (4) or not (2)."""
     import torch
     from sheep_amd import capi, device
 
+    options(part_overlap=ov)
     m, n_ids = 1 << 25, 1 << 20
     rng = np.random.default_rng(3)
     uv = rng.integers(0, n_ids, size=(m, 2), dtype=np.uint32)
