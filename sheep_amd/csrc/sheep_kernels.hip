@@ -1026,6 +1026,103 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
   if (stats) deg_stats_flush(stats, mx, zeros);
 }
 
+// k_degb_hist16 in slices (the fused front pass's histogram): bucket b's entries, x endpoints
+// [xs[b], min(xs[b + 1], xf[b])) then y ids [ys[b], min(ys[b + 1], yf[b])), are cut into
+// ceil(count / CH) slices of CH entries, one workgroup each (block i finds its bucket and slice
+// from a block-wide scan of the slice counts; blocks past the last slice return).  A bucket of
+// one slice stores its degrees; the slices of a split bucket add theirs to deg, which the
+// caller zeroed.  One workgroup per bucket left the step waiting on the buckets of the hub ids
+// and on the last round of buckets over the CUs.  Counting as k_degb_hist16 (u16 halves of
+// 32768 LDS words, segments of at most 65535 entries, u32 totals in registers).
+__global__ void __launch_bounds__(DEGB_THREADS)
+k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __restrict__ xs,
+               const unsigned long long* __restrict__ xf, const uint16_t* __restrict__ ey,
+               const unsigned long long* __restrict__ ys, const unsigned long long* __restrict__ yf,
+               uint32_t NB, uint32_t n_ids, uint64_t CH, uint32_t* __restrict__ deg) {
+  __shared__ uint32_t pk[32768];
+  __shared__ uint32_t wsum[DEGB_THREADS / 64], s_b, s_s, s_n;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // slice table: thread t = bucket t
+  uint64_t nx = 0, ny = 0;
+  uint32_t ns = 0;
+  if ((uint32_t)t < NB) {
+    nx = min(xs[t + 1], xf[t]) - min(xs[t], min(xs[t + 1], xf[t]));
+    ny = min(ys[t + 1], yf[t]) - min(ys[t], min(ys[t + 1], yf[t]));
+    ns = (uint32_t)max((uint64_t)1, (nx + ny + CH - 1) / CH);
+  }
+  const uint32_t incl = wave_incl_scan(ns);
+  if (lane == 63) wsum[w] = incl;
+  if (t == 0) s_b = INV;
+  block_sync();
+  uint32_t add = 0;
+  for (int i = 0; i < w; ++i) add += wsum[i];
+  const uint32_t p0 = add + incl - ns;
+  if ((uint32_t)t < NB && blockIdx.x >= p0 && blockIdx.x < p0 + ns) {
+    s_b = t;
+    s_s = blockIdx.x - p0;
+    s_n = ns;
+  }
+  block_sync();
+  const uint32_t b = s_b;
+  if (b == INV) return;  // (uniform: past the last slice)
+  const uint32_t sl = s_s, nsl = s_n;
+  const uint64_t x0 = xs[b], x1 = max(x0, min(xs[b + 1], xf[b]));
+  const uint64_t y0 = ys[b], y1 = max(y0, min(ys[b + 1], yf[b]));
+  const uint64_t v0 = (uint64_t)sl * CH, v1 = min(v0 + CH, (x1 - x0) + (y1 - y0));
+  uint32_t acc[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) acc[k] = 0;
+  constexpr int V = 4;
+  for (int sg = 0; sg < 2; ++sg) {
+    // this slice's part of segment sg (virtual entries [v0, v1) over x then y)
+    const uint64_t off = sg ? (x1 - x0) : 0, len = sg ? (y1 - y0) : (x1 - x0);
+    const uint64_t a = min(max(v0, off), off + len) - off, e = min(max(v1, off), off + len) - off;
+    if (a >= e) continue;
+    const uint16_t* __restrict__ src = sg ? ey : ex;
+    const uint64_t s0 = (sg ? y0 : x0) + a, s1 = (sg ? y0 : x0) + e;
+    for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
+      const uint64_t g1 = min(g0 + 65535, s1);
+      for (uint32_t i = t; i < 32768; i += DEGB_THREADS) pk[i] = 0;
+      block_sync();
+      for (uint64_t i0 = g0 & ~7ull; i0 < g1; i0 += 8 * V * DEGB_THREADS) {
+        uint4 q[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+          const uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + t);
+          q[u] = i < g1 ? *(const uint4*)(src + i) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+          const uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + t);
+          const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint64_t ik = i + k;
+            const uint32_t v = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            if (ik >= g0 && ik < g1) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
+          }
+        }
+      }
+      block_sync();
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t id = (uint32_t)k * DEGB_THREADS + t;
+        acc[k] += (pk[id >> 1] >> (16 * (id & 1))) & 0xFFFFu;
+      }
+      block_sync();
+    }
+  }
+  const uint64_t base = (uint64_t)b << 16;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const uint64_t id = base + (uint64_t)k * DEGB_THREADS + t;
+    if (id < n_ids) {
+      if (nsl == 1) deg[id] = acc[k];
+      else if (acc[k]) atomicAdd(&deg[id], acc[k]);
+    }
+  }
+}
+
 // SH: local-id bits, NB buckets; false when n_ids is beyond the bucketed path (> 2^26).
 static bool degb_params(uint32_t n_ids, int* SH_out, uint32_t* NB_out) {
   int bits = 0;
@@ -1222,13 +1319,17 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                      part_ws + PW_X, part_shift(n_ids, PD_X));
   if (mark) mark(mark_arg, "front_fused");
   // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
-  if (SH > 15)
-    hipLaunchKernelGGL(k_degb_hist16, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, NB, n_ids, deg,
-                       (const unsigned long long*)bst, stats, DEGB_PLAIN16, (const uint16_t*)ob,
-                       (const unsigned long long*)ys64, (const uint64_t*)nullptr,
-                       (const unsigned long long*)bcur, (const unsigned long long*)ycur);
-  else
+  if (SH > 15) {
+    // slices of about 2m / 1024 entries (at least 2^20): 4 slices per CU over 256 CUs
+    const uint64_t CH = std::max<uint64_t>(1ull << 20, (2 * m + 1023) / 1024);
+    const unsigned grid = (unsigned)(NB + (2 * m + CH - 1) / CH + 1);
+    (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
+    hipLaunchKernelGGL(k_degb_hist16s, dim3(grid), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+                       (const unsigned long long*)bst, (const unsigned long long*)bcur,
+                       (const uint16_t*)ob, (const unsigned long long*)ys64,
+                       (const unsigned long long*)ycur, NB, n_ids, CH, deg);
+    if (stats) launch_deg_stats(deg, n_ids, stats, s);
+  } else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, NB, SH, 1u, n_ids,
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
