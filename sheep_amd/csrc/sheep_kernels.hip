@@ -717,7 +717,8 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
               unsigned long long* ycur, const unsigned long long* __restrict__ ycap,
               unsigned long long* bcur, const unsigned long long* __restrict__ bcap,
               uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc, uint32_t* ovf_y,
-              uint32_t* ovf_x, uint32_t* err, uint32_t* __restrict__ xhist, int shx) {
+              uint32_t* ovf_x, uint32_t* err, uint32_t* __restrict__ xhist, int shx,
+              int xdd /* shx == SH + 2: the x digits come from the x runs */) {
   constexpr int TILE = FF_NT * FF_IT;
   __shared__ uint32_t sa[TILE], sb[TILE];
   __shared__ uint32_t ty[DEGB_NB + 1], tx[DEGB_NB + 1], hxd[PD_X], wsum[2 * (FF_NT / 64)];
@@ -749,13 +750,16 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     const bool loop = r.x == r.y;
     if (file_mode || !loop) lx[k] = atomicAdd(&tx[r.x >> SH], 1u);
     if (loop && selfc) atomicAdd(&selfc[r.x], 1u);
-    atomicAdd(&hxd[part_digit<PD_X>(r.x, shx)], 1u);
+    // x digits of k_part<1> (shx == SH + 2: 4 x buckets per digit, taken from the x runs
+    // below; only the records no x run holds are counted here)
+    if (!xdd || lx[k] == INV) atomicAdd(&hxd[part_digit<PD_X>(r.x, shx)], 1u);
   }
   block_sync();
   // both run tables: exclusive starts in the tile, and the global runs (capacity regions: a y
   // run keeps the part that fits; an x run that does not fit is dropped — either sets its flag)
   {
     const uint32_t c1 = (uint32_t)t < NB ? ty[t] : 0u, c2 = (uint32_t)t < NB ? tx[t] : 0u;
+    if (xdd && c2) atomicAdd(&hxd[t >> 2], c2);
     const uint32_t i1 = wave_incl_scan(c1), i2 = wave_incl_scan(c2);
     if (lane == 63) { wsum[w] = i1; wsum[FF_NT / 64 + w] = i2; }
     unsigned long long g1 = 0, g2 = ~0ull;
@@ -1316,7 +1320,8 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   hipLaunchKernelGGL(k_front_fused, dim3(nt), dim3(FF_NT), 0, s, (const uint2*)uv, m, n_ids,
                      file_mode, SH, NB, oa, ob, ycur, (const unsigned long long*)ycap, bcur,
                      (const unsigned long long*)bcap, ep, selfc, ovf_y, ovf_x, err,
-                     part_ws + PW_X, part_shift(n_ids, PD_X));
+                     part_ws + PW_X, part_shift(n_ids, PD_X),
+                     (int)(part_shift(n_ids, PD_X) == SH + 2));
   if (mark) mark(mark_arg, "front_fused");
   // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
   if (SH > 15) {
@@ -2400,7 +2405,9 @@ __device__ __forceinline__ void search512(const uint32_t* tb, const uint32_t* v,
 
 // IN6 (with PRE): the records are k_part<1>'s packed output; x's digit bits come from the
 // x-digit region starts xst (shx: the digit shift).
-template <bool PRE, int NT, int IT, bool IN6 = false>
+// PK (every rank < 2^26): a staged slot holds bin << 52 | hi << 26 | lo, so the write-out reads
+// its bin instead of searching the tile's run starts for it.
+template <bool PRE, int NT, int IT, bool IN6 = false, bool PK = false>
 __global__ void __launch_bounds__(NT)
 k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
            uint32_t n_rank, uint32_t* err, const uint32_t* __restrict__ bins, uint32_t nb,
@@ -2510,7 +2517,12 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
   block_sync();
 #pragma unroll
   for (int k = 0; k < IT; ++k)
-    if (pk[k] != ~0u) stage[tstart[pk[k] >> 16] + (pk[k] & 0xFFFFu)] = item[k];
+    if (pk[k] != ~0u) {
+      const uint64_t v = PK ? ((uint64_t)(pk[k] >> 16) << 52) | ((item[k] >> 32) << 26) |
+                                  (uint32_t)item[k]
+                            : item[k];
+      stage[tstart[pk[k] >> 16] + (pk[k] & 0xFFFFu)] = v;
+    }
   block_sync();
   // The staged tile in bin order, written with every lane busy: slot j belongs to the last bin
   // whose start is <= j (empty bins share their start with the next one).  (One wave per bin
@@ -2518,9 +2530,15 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
   const uint32_t n_st = tstart[511] + hist[511];
   for (uint32_t j = t; j < n_st; j += NT) {
     uint32_t d;
-    search512<1>(tstart, &j, &d);
+    uint64_t v = stage[j];
+    if (PK) {
+      d = (uint32_t)(v >> 52);
+      v = (((v >> 26) & 0x3FFFFFFull) << 32) | (v & 0x3FFFFFFull);
+    } else {
+      search512<1>(tstart, &j, &d);
+    }
     const unsigned long long g = gbase[d];
-    if (g != ~0ull) out[g + (j - tstart[d])] = stage[j];
+    if (g != ~0ull) out[g + (j - tstart[d])] = v;
   }
 }
 
@@ -2534,8 +2552,10 @@ void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* r
   constexpr int NT = 1024, IT = 8;
   const unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
   const bool in6 = pre && part_ws;
-  auto k = in6 ? k_edge_bin<true, NT, IT, true>
-               : pre ? k_edge_bin<true, NT, IT> : k_edge_bin<false, NT, IT>;
+  const bool pk = n_rank <= (1u << 26);  // ranks < n_seq <= n_rank
+  auto k = in6 ? (pk ? k_edge_bin<true, NT, IT, true, true> : k_edge_bin<true, NT, IT, true>)
+       : pre   ? (pk ? k_edge_bin<true, NT, IT, false, true> : k_edge_bin<true, NT, IT>)
+               : (pk ? k_edge_bin<false, NT, IT, false, true> : k_edge_bin<false, NT, IT>);
   hipLaunchKernelGGL(k, dim3(nt), dim3(NT), 0, s, (const uint2*)uv, m, rank, n_rank, err, bins, nb,
                      cursor, cap_end, out, ovf, in6 ? part_ws + PW_XST : (const uint32_t*)nullptr,
                      part_shift(n_rank, PD_X));
