@@ -15,6 +15,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
+COLS = ("degree_sample", "front_fused", "degree_hist", "degree", "part_first", "sequence",
+        "partition", "edge_pass", "tree_insert")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=26)
@@ -30,8 +34,8 @@ def main():
         device.graph2tree(uv, n_ids)
         torch.cuda.synchronize()
         t = dict(capi.last_timings())
-        rows.append([round(t.get(k, 0), 2) for k in ("degree", "part_first", "sequence", "partition", "edge_pass", "tree_insert")])
-    print(json.dumps({"hwq": os.environ.get("GPU_MAX_HW_QUEUES"), "cols": "degree part_first sequence partition edge_pass tree", "reps": rows[1:]}), flush=True)
+        rows.append([round(t.get(k, 0), 2) for k in COLS])
+    print(json.dumps({"hwq": os.environ.get("GPU_MAX_HW_QUEUES"), "cols": " ".join(COLS), "reps": rows[1:]}), flush=True)
 
 
 if __name__ == "__main__":
