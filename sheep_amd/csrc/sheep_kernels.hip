@@ -158,27 +158,45 @@ void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* 
 }
 
 // stats[0] = max degree, stats[1] = number of zero-degree ids.
+__device__ __forceinline__ void block_sync();
+// Max degree and zero-degree count: 16-B loads when deg is 16-B aligned (V4; else one word per
+// load), one pair of atomics per workgroup.
+template <bool V4>
 __global__ void k_deg_stats(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* stats) {
+  __shared__ uint32_t smx[BLOCK / 64], szr[BLOCK / 64];
   uint32_t mx = 0, zeros = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t d = deg[i];
+  const uint32_t n4 = V4 ? n / 4 : 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const uint4 q = ((const uint4*)deg)[i];
+    mx = max(max(mx, max(q.x, q.y)), max(q.z, q.w));
+    zeros += (q.x == 0) + (q.y == 0) + (q.z == 0) + (q.w == 0);
+  }
+  for (uint32_t i = 4 * n4 + blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t d = deg[i];
     mx = max(mx, d);
-    zeros += (d == 0);
+    zeros += d == 0;
   }
   for (int o = 32; o > 0; o >>= 1) {
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     zeros += (uint32_t)__shfl_xor((int)zeros, o);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(&stats[0], mx);
-    atomicAdd(&stats[1], zeros);
+  if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = mx; szr[threadIdx.x >> 6] = zeros; }
+  block_sync();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < BLOCK / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; }
+    if (mx) atomicMax(&stats[0], mx);
+    if (zeros) atomicAdd(&stats[1], zeros);
   }
 }
 
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats, hipStream_t s) {
   (void)hipMemsetAsync(stats, 0, 8, s);
   if (n == 0) return;
-  hipLaunchKernelGGL(k_deg_stats, dim3(grid_for(n)), dim3(BLOCK), 0, s, deg, n, stats);
+  const bool v4 = ((uintptr_t)deg & 15) == 0;
+  hipLaunchKernelGGL(v4 ? k_deg_stats<true> : k_deg_stats<false>,
+                     dim3(std::min<unsigned>(grid_for(v4 ? n / 4 + 1 : n), 1024)), dim3(BLOCK), 0, s,
+                     deg, n, stats);
 }
 
 __global__ void k_fill(uint32_t* p, uint32_t v, uint64_t n) {
