@@ -3353,7 +3353,7 @@ static constexpr uint32_t KM_FLUSH = 65535 / KM_CHUNK;  // chunks per window flu
 // ~80 KB, so map + summary stays one block per CU and leaves ~16 KB beside it for the zipper.
 static constexpr uint32_t KM_GSUM = 16384;
 
-template <bool STATS>
+template <bool STATS, bool HUB = false>
 __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, KbSegs sg,
          uint32_t B0, int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
@@ -3469,6 +3469,13 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     uint32_t bbase, gend;
     window(nh0, nbl, bbase, gend);
     const uint32_t span = gend - bbase;  // ranks of the window that can hold records
+    // Narrow windows (hub bins: few ranks, many records each) keep RF u32 copies of each
+    // rank's count, lane l adding to copy l % RF: a hub's lanes in one wave then hit RF
+    // addresses, not one (same-address LDS atomics of a wave serialise).  RF = 1: the packed
+    // 16-bit counts.  (RF is fixed per window: the window, hence span, only changes at a flush.)
+    // HUB: buckets of 2^25 records and more (launch_kb_map; the small configs keep the plain
+    // counts: with the copies their tree took 0.1-0.15 ms longer).
+    const uint32_t RF = !HUB ? 1u : span <= 512 ? 32u : span <= 1024 ? 16u : span <= 2048 ? 8u : 1u;
     uint32_t gw[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -3540,8 +3547,9 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       if (STATS) { edges += valid; kept_n += valid && !gi; inb += valid && !gi && a >= B0; }
       const uint32_t o = b - bbase;
       if (valid && cnt) {
-        if (o < span) atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
-        else atomicAdd(&cnt[b], 1u);
+        if (o >= span) atomicAdd(&cnt[b], 1u);
+        else if (RF > 1) atomicAdd(&wcnt[o * RF + (lane & (RF - 1))], 1u);
+        else atomicAdd(&wcnt[o >> 1], 1u << (16 * (o & 1)));
       }
       if (gi) {  // a hub's records repeat its mark: test first (a read of one word is a
                  // broadcast, same-word atomics from a wave serialise)
@@ -3557,7 +3565,9 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     }
     if (lane == 0) woff[w] = nout;
     // flush the window unless the next chunk of this block keeps it (uniform decision)
-    bool flush = !more || ++since_flush >= KM_FLUSH;
+    // (the packed 16-bit counts must not carry: flushed every KM_FLUSH chunks; the u32 copies
+    // only when the window changes)
+    bool flush = !more || (++since_flush >= KM_FLUSH && RF == 1);
     if (!flush) {
       uint32_t nbase, nend;
       window(nh0, nbl, nbase, nend);
@@ -3573,7 +3583,16 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
           wbits[i] = 0;
         }
       }
-      if (cnt)
+      if (cnt && RF > 1) {
+        for (uint32_t i = t; i < span; i += KM_THREADS) {
+          uint32_t v = 0;
+          for (uint32_t r = 0; r < RF; ++r) {
+            v += wcnt[i * RF + r];
+            wcnt[i * RF + r] = 0;
+          }
+          if (v) atomicAdd(&cnt[bbase + i], v);
+        }
+      } else if (cnt) {
         for (uint32_t i = t; i < (span + 1) / 2; i += KM_THREADS) {
           const uint32_t v = wcnt[i];
           if (v) {
@@ -3582,6 +3601,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
             wcnt[i] = 0;
           }
         }
+      }
     }
     // compaction: one reservation per chunk for the kept pairs of all its waves
     if (t == 0) {
@@ -4014,7 +4034,9 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   // this map, and more map blocks slow it down more than they speed the map up (RMAT-26 tree
   // phase 28.6 / 27.6 / 31.0 / 29.8 ms at 512 / 256 / 320 / 384 blocks; 192: 29.7).
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
-  auto mk = stats ? k_kb_map<true> : k_kb_map<false>;
+  const bool hub = e_end - e_begin >= (1ull << 25);
+  auto mk = stats ? (hub ? k_kb_map<true, true> : k_kb_map<true, false>)
+                  : (hub ? k_kb_map<false, true> : k_kb_map<false, false>);
   // the giant summary of the highest KM_GSUM words of ranks below B0 (the lo ends of most
   // records: a vertex is the lo end of its edges to higher-degree vertices) in dynamic LDS
   const uint32_t w_end = (B0 + 2047) / 2048;
