@@ -235,7 +235,9 @@ std::unique_ptr<Comm> local_comm(std::shared_ptr<LocalGroup> g, int rank) {
 // of a test box): each rank stages its buffer in its slot of a POSIX shared-memory region, a
 // process-shared barrier orders the ranks, and each rank combines the slots on the host.
 // Synchronous (the stream is drained first), chunked by the slot size.  Tests only: the bytes
-// cross PCIe twice.
+// cross PCIe twice.  A group's name must be unique to the group (the tests use uuids): rank 0
+// unlinks a crashed run's region of the same name before creating its own, but a rank that
+// opened the old one first would attach to it and wait at its barrier.
 struct ShmHeader {
   pthread_barrier_t bar;
   std::atomic<uint32_t> ready;
