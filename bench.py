@@ -46,10 +46,15 @@ def pmc_traffic(kernel, key):
     try:
         tab = json.load(open(path))[key]
         base, _, targ = kernel.partition("<")  # "k_part<1>" matches "k_part<1, 512, 16>"
-        for k, rec in tab.items():
+        byts = launches = 0
+        for k, rec in tab.items():  # every template variant of the kernel (e.g. the map's hub one)
             kb, _, kt = k.replace("sheep::", "").partition("<")
             if kb == base and (not targ or kt.split(",")[0].rstrip(">").strip() == targ.rstrip(">")):
-                return rec["hbm_bytes_per_launch"]
+                n = rec.get("launches", 1)
+                byts += rec["hbm_bytes_per_launch"] * n
+                launches += n
+        if launches:
+            return byts / launches
     except (OSError, KeyError, ValueError):
         pass
     return None
