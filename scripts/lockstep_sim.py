@@ -38,6 +38,9 @@ def main():
     seq, parent, pst, n = device.graph2tree(uv, n_ids)
     ref = (seq[:n].clone(), parent[:n].clone(), pst[:n].clone())
     single = dict(capi.last_timings())
+    # pairs that linked two components over the whole loop (parent != INVALID): the floor of
+    # what any per-rank spanning-forest pre-reduction could leave of the exchanged pairs
+    tree_edges = int(((ref[1].to(torch.int64) & 0xFFFFFFFF) != 0xFFFFFFFF).sum())
     del seq, parent, pst
     for P in args.P:
         shards = [uv[slice(*shard_bounds(m, r, P))] for r in range(P)]
@@ -59,6 +62,7 @@ def main():
                    "zip_ms_per_rank": [round(x, 3) for x in st.get("kb_zip", [])],
                    "apply_ms_per_rank": [round(x, 3) for x in st["kb_apply"]],
                    "kept_pairs": st.get("kept", 0), "gathered_pairs": st.get("gathered", 0),
+                   "tree_edges": tree_edges,
                    "K": os.environ.get("SHEEP_KB_BUCKETS", "auto"),
                    "single_gpu_tree_insert_ms": round(single.get("tree_insert", 0), 3)}
             if best is None or rec["critical_tree_ms"] < best["critical_tree_ms"]:
