@@ -233,6 +233,29 @@ def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, options, n, m, mode):
     assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("n,mode", [(3000017, 0), (40000003, 1)])
+def test_graph2tree_dev_fused_ragged_ids(oracle, gpu, n, mode):
+    """The default front half (the fused pass, sampled capacities) on id spaces that are not a
+    power of two: 733 degree buckets of 4K ids (n = 3,000,017) or 611 of 64K ids (n =
+    40,000,003), each with a ragged last bucket and y digit, over 2^25 + 999 power-law records
+    (a ragged last tile): seq, parent and pst bit-exact in both degree conventions."""
+    import torch
+    from sheep_amd import capi, device
+
+    m = (1 << 25) + 999
+    uv_d = device.powerlaw(n, m, 2.2, 80.0, 40 + mode)
+    s_d, p_d, w_d, k = device.graph2tree(uv_d, n, mode)
+    torch.cuda.synchronize()
+    assert "front_fused" in dict(capi.last_timings())
+    uv = uv_d.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    seq = oracle.degree_sequence(uv, mode)
+    p, w = oracle.build_tree(uv, seq)
+    assert k == len(seq)
+    assert np.array_equal(s_d[:k].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:k].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("n,m,gamma,i0,seed", [(1000, 20000, 2.3, 100.0, 3),
                                                (65536, 1 << 20, 2.1, 50.0, 5),
                                                (300001, 1 << 21, 2.3, 100.0, 7)])
