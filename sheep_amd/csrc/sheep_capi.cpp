@@ -685,8 +685,10 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 // The cuts as bin indices (sorted, distinct, in (0, nb - 1)).
 static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                                          const std::vector<unsigned long long>& bin_start,
-                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 40) {
+                                         uint64_t m, uint32_t n_seq, uint32_t kmax = 40,
+                                         int merge = -1 /* kb_merge; -1: the option */) {
   const uint32_t nb = (uint32_t)bounds.size();
+  if (merge < 0) merge = knobs().kb_merge;
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
   kb_counts(m, &K_e, &K_r, kmax);
@@ -705,8 +707,8 @@ static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
   }
   std::sort(cuts.begin(), cuts.end());
   cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
-  if (knobs().kb_merge > 0) {  // lab: drop a cut while the buckets either side hold few records
-    const uint64_t thr = m_valid * (uint64_t)knobs().kb_merge / 10000;
+  if (merge > 0) {  // drop a cut while the buckets either side hold few records
+    const uint64_t thr = m_valid * (uint64_t)merge / 10000;
     std::vector<uint32_t> kept;
     uint32_t prev = 0;
     for (size_t i = 0; i < cuts.size(); ++i) {
@@ -1222,7 +1224,10 @@ static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_ou
     *ms_out = 0;
     return;
   }
-  std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq, 40);
+  // the lockstep loop merges at 0.2 %: at the one-GPU loop's 0.35 % the giant of RMAT-26 forms
+  // where the P = 8 simulation's tree critical path goes 6.7 -> 16.4 ms
+  std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq, 40,
+                                           knobs().kb_merge > 0 ? 20 : 0);
   std::vector<uint32_t> bi;  // bin index at each bucket start, then nb - 1 (the INVALID bin)
   bi.push_back(0);
   for (uint32_t i : cuts) bi.push_back(i);

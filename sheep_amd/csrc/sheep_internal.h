@@ -55,7 +55,8 @@ struct Knobs {
   int ls_split = 1;      // SHEEP_LS_SPLIT: with P > 1 ranks each bucket's zipper runs on one owner
                          //   rank (0: every rank applies every bucket's zipper)
   int kb_merge = 35;     // SHEEP_KB_MERGE: merge adjacent kb buckets while together they hold at
-                         //   most kb_merge / 10000 of the records (0: off)
+                         //   most kb_merge / 10000 of the records (0: off;
+                         //   the lockstep loop: 20 unless off)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
