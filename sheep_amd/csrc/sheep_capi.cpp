@@ -526,8 +526,27 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   const bool pipe = knobs().kb_pipe && !per_bucket && 2 * max_e <= m;
   uint64_t* kept[2] = {spare, pipe ? spare + m / 2 : spare};
   auto par = [&](size_t k) { return pipe ? (int)(k & 1) : 0; };
+  // Fresh anchors around the giant's birth.  A pipelined map anchors on the state before the
+  // previous bucket's apply, so the bucket after the one where the giant forms is mapped
+  // against a component that is not the giant yet, and its zipper walks the new giant's chains
+  // without the spine rules (RMAT-26 seed 5: tree 19.7 ms, 14.8 with a fresh anchor).  Where
+  // that happens is estimated from the records: the mean degree 2E/B of the graph on the ranks
+  // below a bucket's end crossing 1/2 to 1.  Each bucket after such a bucket is mapped after the
+  // previous apply (anchored on it), not beside it.  Tree ms, default -> fresh: RMAT-26 seed 26
+  // 14.8 -> 15.0, seed 5 19.7 -> 15.1, RMAT-25 seed 9 11.5 -> 9.6, RMAT-24 7.1 -> 6.2, RMAT-22
+  // 3.07 -> 2.64, twitter shape 21.8 -> 21.1 (profiles/r04/ak_fresh_anchor/).
+  std::vector<char> fresh(nbk + 1, 0);
+  if (pipe) {
+    double E = 0;
+    for (size_t k = 0; k + 1 < nbk; ++k) {
+      E += (double)recs(k);
+      const double B = (double)bk[k + 1].first, d = B > 0 ? 2.0 * E / B : 0.0;
+      if (d >= 0.5) fresh[k + 1] = 1;
+      if (d >= 1.0) break;
+    }
+  }
   auto anchor_of = [&](size_t k) -> uint32_t {
-    size_t a = pipe ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
+    size_t a = pipe && !fresh[k] ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
     return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
   };
   // The giant bitmap's reference vertex lives in slot j & 1 for map j: the rebase before map
@@ -583,15 +602,17 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     size_t slot = 0;
     for (size_t k = 0; k < nbk; ++k) {
       HIP_CHECK(hipStreamWaitEvent(sa, ev_map[k & 1], 0));
-      if (k + 1 < nbk) {
+      auto next = [&]() {
         rebase(k + 1);
         slot = k + 1;
         HIP_CHECK(hipEventRecord(ev_reb[k & 1], sa));
         HIP_CHECK(hipStreamWaitEvent(s2, ev_reb[k & 1], 0));
         map_k(k + 1, s2);
         HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
-      }
+      };
+      if (k + 1 < nbk && !fresh[k + 1]) next();
       apply_k(k, slot, sa);
+      if (k + 1 < nbk && fresh[k + 1]) next();
     }
     if (sa != s) {  // s resumes after the last apply
       HIP_CHECK(hipEventRecord(c.kb_ev[4], sa));
