@@ -39,9 +39,12 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def pmc_traffic(kernel, key):
+def pmc_traffic(kernel, key, field="hbm_bytes_per_launch_fetch_x2"):
     """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/), if one was
-    collected for this workload: FETCH_SIZE and WRITE_SIZE from separate rocprofv3 --pmc passes."""
+    collected for this workload: FETCH_SIZE and WRITE_SIZE from separate rocprofv3 --pmc passes.
+    The default field is the corrected one (MI355X_MICROARCH.md, HBM/rocprofv3: on gfx950
+    FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so FETCH is doubled);
+    "hbm_bytes_per_launch" is the raw FETCH + WRITE."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         tab = json.load(open(path))[key]
@@ -51,7 +54,7 @@ def pmc_traffic(kernel, key):
             kb, _, kt = k.replace("sheep::", "").partition("<")
             if kb == base and (not targ or kt.split(",")[0].rstrip(">").strip() == targ.rstrip(">")):
                 n = rec.get("launches", 1)
-                byts += rec["hbm_bytes_per_launch"] * n
+                byts += rec[field] * n
                 launches += n
         if launches:
             return byts / launches
@@ -257,6 +260,7 @@ def main():
             roof = {"kernel": name, "bound": "hbm", "achieved": ach / 1e9,
                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
                     "traffic": pmc_traffic(name, key), "algo_bytes": algo / launches,
+                    "traffic_raw": pmc_traffic(name, key, "hbm_bytes_per_launch"),
                     "io_bytes": io / launches, "io_GB_s": io / (ms * 1e-3) / 1e9,
                     "avg_ms": per_launch_ms, "launches_per_step": launches,
                     "ms_per_step": ms,

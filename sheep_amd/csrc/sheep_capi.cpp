@@ -246,6 +246,13 @@ struct Timer {
   }
 };
 
+// The walk guards' fault bits (sheep_kernels.hip FAULT_*).
+static const char* fault_text(uint32_t f) {
+  return (f & 1) ? "forest not heap-ordered"
+         : (f & 4) ? "kept pairs past their buffer"
+                   : "union-find cycle";
+}
+
 // Read and clear the device error word (synchronises s).
 static void check_err(Ctx& c, hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(c.h_pinned, c.d_err, 4, hipMemcpyDeviceToHost, s));
@@ -257,8 +264,7 @@ static void check_err(Ctx& c, hipStream_t s) {
     const uint32_t f = c.h_pinned[12];
     HIP_CHECK(hipMemsetAsync(fw, 0, 4, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    throw ApiError(-EIO, std::string("device walk guard tripped (") +
-                             ((f & 1) ? "forest not heap-ordered" : "union-find cycle") +
+    throw ApiError(-EIO, std::string("device walk guard tripped (") + fault_text(f) +
                              "): corrupt intermediate data");
   }
   if (e) {
@@ -292,8 +298,7 @@ static void check_err_group(Ctx& c, Comm& comm, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
   const uint32_t f = (uint32_t)(h >> 32), e = (uint32_t)h;
   if (f)
-    throw ApiError(-EIO, std::string("device walk guard tripped on a rank (") +
-                             ((f & 1) ? "forest not heap-ordered" : "union-find cycle") +
+    throw ApiError(-EIO, std::string("device walk guard tripped on a rank (") + fault_text(f) +
                              "): corrupt intermediate data");
   if (e & ERR_DUP_SEQ) throw ApiError(-EINVAL, "sequence repeats a vertex id");
   throw ApiError(-ERANGE, "vertex id out of range of the sequence/id space");
@@ -575,11 +580,17 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     }
     launch_kb_map(sorted, seg ? seg->cstart[bk[k].second] : bk[k].second,
                   seg ? seg->cstart[bk[k + 1].second] : bk[k + 1].second, bk[k].first,
-                  anchor_of(k), uf, label, kept[p], bitmaps + p * bm_words, counters + p * 16,
+                  anchor_of(k), uf, label, kept[p], pipe ? m / 2 : m, bitmaps + p * bm_words,
+                  counters + p * 16,
                   lo_bit, hcnt, stats, ws, bins, nb, gbits, gbits ? gx + (k & 1) : nullptr, 1,
                   st, seg ? &sg : nullptr, anc ? anc + (k & 1) : nullptr, k >= 1 ? gsum : nullptr);
     if (tm) tm->span_end(sp, st);
   };
+  // anc_next: the union keeps the root of the next map's anchor on top, so that the map running
+  // beside it sees the giant's root unchanged.  When map k+1 is fresh (fresh[k+1]), the apply runs
+  // before rebase(k+1), so that slot still holds the anchor picked for map k-1: nothing maps
+  // beside this union then, and keeping that (after the birth: the giant's) root on top is
+  // harmless (ADVICE r04 noted the stale slot).
   auto apply_k = [&](size_t k, size_t slot, hipStream_t st) {
     int p = par(k);
     launch_kb_apply(recs(k) > 0, bk[k].first, bk[k + 1].first, anchor_of(k),
@@ -818,6 +829,24 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     }
     src = (const uint32_t*)items_b;
     if (tm) tm->mark("partition");
+  }
+  if (!direct && part && di && di->part_first_done && di->mid_caps) {
+    // The first pass wrote capacity regions (launch_front_fused / launch_part_first_caps) whose
+    // overflow word the direct branch reads with the bins' own; without direct binning (n_seq
+    // <= 256, or bin_direct 0) it is read here: an overflowed region lost records, so the
+    // partition is run again from the records.
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 10, c.d_err + 3, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c.h_pinned[10]) {
+      DegInfo d2 = *di;
+      d2.part_first_done = false;
+      d2.mid_caps = false;
+      d2.mid_p6 = false;
+      d2.mid_slots = 0;
+      d2.yhist_ready = false;
+      build_tree_dev(c, d_uv, m, d_rank, n_rank, n_seq, d_parent, d_pst, s, tm, &d2, allow_direct);
+      return;
+    }
   }
   const uint64_t* sorted;
   uint64_t* spare;
@@ -1060,11 +1089,15 @@ struct Lockstep {
 // part_done (nullable): the first partition pass of the rank gathers was launched by the caller
 // into "ls_items" (with "part_ws" holding its cursors) and completes at this event.
 // nsd (nullable): the global degrees in sequence order, read instead of d_deg[d_seq[r]].
+// mid_caps: the first pass wrote capacity regions of mid_slots records (launch_front_fused,
+// packed: mid_p6) whose overflow word is d_err[3]; an overflow sends this rank's partition
+// back to the unpacked records (as build_tree_dev does).
 static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32_t* d_rank,
                      uint32_t n_rank, const uint32_t* d_seq, uint32_t n_seq,
                      const uint32_t* d_deg, uint64_t* counts_out, uint32_t* nb_out,
                      uint32_t* d_err, hipStream_t s, hipEvent_t part_done = nullptr,
-                     const uint32_t* nsd = nullptr, bool ids_checked = false) {
+                     const uint32_t* nsd = nullptr, bool ids_checked = false,
+                     uint64_t mid_slots = 0, bool mid_caps = false, bool mid_p6 = false) {
   require_records(m, "lockstep");
   Scratch& sc = *L.scp;
   L.m = m;
@@ -1142,8 +1175,10 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     if (part_done) {  // pass 1 ran beside the degree all-reduce and the sequence
       pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
       HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
-      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6);
+      launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6, mid_slots, mid_caps,
+                         mid_p6);
     } else {
+      mid_caps = false;
       pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, false, pre6);
     }
@@ -1156,6 +1191,8 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
   const uint32_t nb = (uint32_t)L.bounds.size();
   L.bins = (uint32_t*)sc.get("ls_bins", 512 * 4);
   HIP_CHECK(hipMemcpyAsync(L.bins, L.bounds.data(), nb * 4, hipMemcpyHostToDevice, s));
+  mid_caps = mid_caps && part && part_done;
+  bool part_ovf = false, part_checked = false;
   // Direct binning, as the one-GPU path: this shard's share of each bin's estimate (the bins
   // and estimates are global) sizes its capacity; a bin that outgrows it sends this rank
   // through the scatter below (ranks may differ in that: only per-bin counts are exchanged).
@@ -1182,8 +1219,12 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
     std::vector<unsigned long long> cur(nb);
     HIP_CHECK(hipMemcpyAsync(cur.data(), L.dseg + 512, nb * 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(L.h_pinned, ovf, 4, hipMemcpyDeviceToHost, s));
+    L.h_pinned[1] = 0;
+    if (mid_caps) HIP_CHECK(hipMemcpyAsync(L.h_pinned + 1, d_err + 3, 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (L.h_pinned[0] == 0) {
+    part_checked = true;
+    part_ovf = mid_caps && L.h_pinned[1] != 0;
+    if (L.h_pinned[0] == 0 && !part_ovf) {
       L.direct = true;
       L.sorted = binned;
       for (uint32_t i = 0; i + 1 < nb; ++i) counts_out[i] = cur[i] - L.cstart[i];
@@ -1192,7 +1233,14 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
       return;
     }
   }
-  if (pre6) {  // a bin overflowed: the scatter path reads unpacked records, so partition again
+  if (mid_caps && !part_checked) {  // (no direct binning: the regions' overflow word alone)
+    HIP_CHECK(hipMemcpyAsync(L.h_pinned + 1, d_err + 3, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    part_ovf = L.h_pinned[1] != 0;
+  }
+  // A bin overflowed (the scatter path reads unpacked records), or a capacity region of the
+  // first pass did (its records are incomplete): partition again from the records.
+  if (pre6 || part_ovf) {
     uint32_t* pws2 = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
     launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws2, s, false, false);
   }
@@ -1279,9 +1327,12 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   if (L.direct)
     sg = {L.dseg, L.dseg + 512, L.dseg + 1024, (uint32_t)L.bk[k].second,
           (uint32_t)L.bk[k + 1].second};
-  launch_kb_map(L.sorted, L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second,
-                L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second, B0, L.anchor(k),
-                L.uf, L.label, d_send + L.ms, L.bm_of(k), L.cnt_of(k), 0, L.hcnt, false, L.ws,
+  // (d_send holds ms mark words + one pair per record of the bucket: the caller's contract)
+  const uint64_t e0 = L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second;
+  const uint64_t e1 = L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second;
+  launch_kb_map(L.sorted, e0, e1, B0, L.anchor(k),
+                L.uf, L.label, d_send + L.ms, e1 - e0, L.bm_of(k), L.cnt_of(k), 0, L.hcnt,
+                false, L.ws,
                 L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
                 L.split ? 2 : (int)L.defer, s, L.direct ? &sg : nullptr,
                 L.anc ? L.anc + (k & 1) : nullptr,
@@ -1492,6 +1543,8 @@ static uint32_t sequence_sharded(Ctx& c, Comm& comm, const uint32_t* deg_local, 
     uint32_t* nsd = (uint32_t*)sc.get("sq_nsd", (size_t)n_seq * 4);
     const uint32_t n2 = sequence_dev(c, dall, n_ids, d_seq, rank, s, false, nsd);
     if (n2 != n_seq) throw ApiError(-EIO, "sharded sequence: id counts disagree");
+    // rank holds n_pad words, INVALID past the id space (as the sharded path's fill + gather)
+    if (n_pad > n_ids) launch_fill(rank + n_ids, INV, n_pad - n_ids, s);
     *nsd_out = nsd;
     return n_seq;
   }
@@ -1542,13 +1595,44 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   uint32_t* selfc = (uint32_t*)c.scratch.get("mt_selfc", n * 4);
   uint32_t* deg = (uint32_t*)c.scratch.get("mt_deg", n * 4);
   uint32_t* rank = (uint32_t*)c.scratch.get("mt_rank", n * 4);
-  // the first partition pass of the rank gathers needs no ranks: it runs on the side stream
-  // beside the rest of the degree pass, the degree all-reduce and the sequence sort
-  const bool overlap = knobs().part_overlap != 0 && m > 0 && use_part(m);
+  // The front half of this rank's shard, as graph2tree_dev's: from 2^25 records ONE read of the
+  // shard gives its degrees and the first partition pass of the rank gathers, packed into
+  // sampled capacity regions (launch_front_fused; part_overlap 4).  Else the first pass, which
+  // needs no ranks, runs on the side stream beside the degree pass, the degree collectives and
+  // the sequence.
+  const int ov = knobs().part_overlap;
+  const bool ffused = ov == 4 && m >= (1ull << 25) && use_part(m) && knobs().bin_direct &&
+                      knobs().degree != 1 && part_p6_ok(n_ids) && front_fused_ok(m, n_ids) &&
+                      degs_tmp_words(m, n_ids) > 1;
+  const uint64_t mid_slots = ffused ? (fs_room(m, 1024) + 7) & ~7ull : m;
+  const bool overlap = !ffused && ov != 0 && m > 0 && use_part(m);
   hipEvent_t part_done = nullptr;
+  if (ffused) {
+    uint32_t* ovf_deg = c.d_err + 2;
+    HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words ([3]: the partition's)
+    uint32_t* tmp = (uint32_t*)c.scratch.get("degs_tmp", degs_tmp_words(m, n_ids) * 4);
+    uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
+    // (at least m u64: ls_begin takes the same buffer at that size and must not regrow it)
+    uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", std::max<uint64_t>(m, mid_slots) * 8);
+    uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
+    launch_front_fused(d_uv, m, n_ids, mode, deg_local, selfc, c.d_err, tmp, pws, mid, mid_slots,
+                       stats, ovf_deg, c.d_err + 3, s);
+    HIP_CHECK(hipEventRecord(c.part_ev[1], s));
+    part_done = c.part_ev[1];
+    // this shard's degrees are complete unless an x bucket outgrew its region (a local
+    // decision: the exact pass has no collectives)
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (tm) tm->mark("front_fused");
+    if (c.h_pinned[4]) {
+      degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s);
+      if (tm) tm->mark("degree_exact");
+    }
+  }
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
-  const bool yh = degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s, overlap,
-                             overlap ? c.part_ev[0] : nullptr);
+  const bool yh = ffused ? false
+                         : degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s, overlap,
+                                      overlap ? c.part_ev[0] : nullptr);
   if (overlap) {
     uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", m * 8);
     uint32_t* pws = (uint32_t*)c.scratch.get("part_ws", PART_WS_WORDS * 4);
@@ -1573,7 +1657,9 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
       launch_rank_scatter(d_seq, n_seq, rank, c.d_err, s);
     }
   }
-  check_err(c, s);
+  // a range error of any rank's degree pass fails every rank here, after the same collectives
+  // (a rank throwing alone would leave the others waiting in the next one)
+  check_err_group(c, comm, s);
   if (tm) tm->mark("sequence");
   // the lockstep session keeps its buffers in this context's scratch
   Lockstep L;
@@ -1585,9 +1671,9 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   std::vector<uint64_t> counts(513, 0);
   uint32_t nb = 0;
   ls_begin(L, d_uv, m, rank, n_ids, d_seq, n_seq, deg, counts.data(), &nb, c.d_err, s, part_done,
-           nsd, true);
+           nsd, true, mid_slots, ffused, ffused);
   if (part_done) HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));  // also when no tree is built
-  check_err(c, s);
+  check_err_group(c, comm, s);
   uint64_t* dcounts = (uint64_t*)c.scratch.get("mt_counts", 513 * 8);
   HIP_CHECK(hipMemcpyAsync(dcounts, counts.data(), (size_t)nb * 8, hipMemcpyHostToDevice, s));
   comm.allreduce_sum_u64(dcounts, nb, s);

@@ -248,9 +248,10 @@ void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* r
 // One kb bucket in two halves (sheep_kernels.hip): the map (records -> kept pairs + giant marks
 // + hi counts) and the apply (spine, zipper, union-find fold, labels).  counters: this
 // bucket parity's 4 words; anchor: see launch_kb_map.
+// kept_cap: the u64 slots kept holds (a reservation past it raises the fault word, -EIO).
 void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
-                   uint32_t* bitmap, uint32_t* counters, int gshift,
+                   uint64_t kept_cap, uint32_t* bitmap, uint32_t* counters, int gshift,
                    uint32_t* cnt /* nullable: hi run lengths */, bool stats,
                    unsigned long long* st, const uint32_t* bins /* nullable: hi bins */,
                    uint32_t nb, uint32_t* gbits /* nullable: giant bitmap */,

@@ -52,7 +52,7 @@ static unsigned device_cus() {
 __device__ uint32_t g_fault;
 static constexpr uint32_t FAULT_STEPS = 1u << 26;
 __device__ __forceinline__ void raise_fault(uint32_t bit) { atomicOr(&g_fault, bit); }
-constexpr uint32_t FAULT_FOREST = 1u, FAULT_UF = 2u;
+constexpr uint32_t FAULT_FOREST = 1u, FAULT_UF = 2u, FAULT_KEPT = 4u;
 
 uint32_t* fault_word() {
   void* p = nullptr;
@@ -3360,7 +3360,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
          uint32_t* n_kept, uint32_t* bitmap, uint32_t* cnt, unsigned long long* stats,
          uint32_t anchor, const uint32_t* __restrict__ bins, uint32_t nb, uint32_t* gbits,
          const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc,
-         const uint32_t* __restrict__ gsum, uint32_t gs_words, uint32_t gs_w0) {
+         const uint32_t* __restrict__ gsum, uint32_t gs_words, uint32_t gs_w0, uint32_t kept_cap) {
   extern __shared__ uint32_t s_gsum[];  // gs_words words of the giant summary (dynamic LDS)
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
@@ -3603,18 +3603,28 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
         }
       }
     }
-    // compaction: one reservation per chunk for the kept pairs of all its waves
+    // compaction: one reservation per chunk for the kept pairs of all its waves.  Guard: a
+    // chunk keeps at most its records and the host sizes kept for the bucket's records, so a
+    // reservation past kept_cap means corrupt counts; it raises the fault word (-EIO), nothing
+    // is written past kept_cap, and n_kept is clamped to it (every later reservation is past it
+    // too and clamps again), so the refresh and the zipper read only written slots.
     if (t == 0) {
       uint32_t run = 0;
       for (int i = 0; i < KM_THREADS / 64; ++i) { uint32_t v = woff[i]; woff[i] = run; run += v; }
-      woff[KM_THREADS / 64] = run ? atomicAdd(n_kept, run) : 0u;
+      const uint32_t base = run ? atomicAdd(n_kept, run) : 0u;
+      if (run && (uint64_t)base + run > kept_cap) {
+        raise_fault(FAULT_KEPT);
+        atomicMin(n_kept, kept_cap);
+      }
+      woff[KM_THREADS / 64] = base;
     }
     block_sync();
     uint32_t pos = woff[KM_THREADS / 64] + woff[w];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       uint64_t bal = __ballot(it[r] != ~0ull);
-      if (it[r] != ~0ull) kept[pos + __popcll(bal & lt)] = it[r];
+      const uint32_t q = pos + (uint32_t)__popcll(bal & lt);
+      if (it[r] != ~0ull && q < kept_cap) kept[q] = it[r];
       pos += (uint32_t)__popcll(bal);
     }
     // no barrier here: the next chunk writes LDS only after its own barrier has seen every
@@ -4018,7 +4028,7 @@ void launch_kb_bounds(const uint64_t* items, uint64_t n, uint32_t K_e, uint32_t 
 // launch_gb_rebase wrote before this map.
 void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint32_t B0,
                    uint32_t anchor, uint32_t* uf, const uint32_t* label, uint64_t* kept,
-                   uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
+                   uint64_t kept_cap, uint32_t* bitmap, uint32_t* counters, int gshift, uint32_t* cnt, bool stats,
                    unsigned long long* st, const uint32_t* bins, uint32_t nb, uint32_t* gbits,
                    const uint32_t* gx, int defer, hipStream_t s, const KbSegs* segs,
                    const uint32_t* anc, const uint32_t* gsum) {
@@ -4044,7 +4054,8 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   const uint32_t gs_w0 = w_end - gs_words;
   hipLaunchKernelGGL(mk, dim3(grid), dim3(KM_THREADS), gs_words * 4, s, items, e_begin, e_end, sg,
                      B0, gshift, uf, label, kept, counters + 3, bitmap, cnt, st, anchor, bins, nb,
-                     gx ? gbits : nullptr, gx, defer, anc, gsum, gs_words, gs_w0);
+                     gx ? gbits : nullptr, gx, defer, anc, gsum, gs_words, gs_w0,
+                     (uint32_t)std::min<uint64_t>(kept_cap, 0xFFFFFFFFull));
 }
 
 void launch_kb_pick(const uint32_t* uf, uint32_t B0lim, const uint32_t* anc_prev, uint32_t* anc_out,

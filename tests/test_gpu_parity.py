@@ -210,6 +210,33 @@ def test_graph2tree_dev_sampled_capacities_overflow(oracle, gpu, options, ov):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("ov", [4, 2])
+def test_graph2tree_dev_sampled_overflow_few_ids(oracle, gpu, options, ov):
+    """The sampled regions overflow on an input with at most 256 ids in use: the
+    tree then takes no hi bins (n_seq <= 256), so the direct edge pass, which used to be the
+    only reader of the first pass's overflow word, does not run.  Every 256th record (the
+    sampled ones) joins ids 0 and 1, the others join 200 ids spread over 2^20 (one per y digit,
+    none of which the sample saw).  Bit-exact, fused (4) or not (2)."""
+    import torch
+    from sheep_amd import device
+
+    options(part_overlap=ov)
+    m, n_ids = 1 << 25, 1 << 20
+    rng = np.random.default_rng(4)
+    ids = (np.arange(1, 201, dtype=np.uint32) * 5003) % n_ids
+    uv = ids[rng.integers(0, ids.size, size=(m, 2))]
+    uv[::256] = (0, 1)
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, n_ids)
+    torch.cuda.synchronize()
+    seq = oracle.degree_sequence(uv)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq) <= 256
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("n,m,mode", [((1 << 26) + 5, (1 << 22) + 12345, 0),
                                       ((1 << 25) + 77, (1 << 22) + 1, 1)])
 def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, options, n, m, mode):
