@@ -68,6 +68,18 @@ def main():
             if best is None or rec["critical_tree_ms"] < best["critical_tree_ms"]:
                 best = rec
             del s, p, w
+        # The per-rank front half, measured: rank 0's shard through the one-GPU path over the
+        # global id space (the front half multi_tree runs per shard from 2^25 records: the fused
+        # one-read pass, the histogram, the second partition pass and the edge pass; its local
+        # sequence stands in for the sharded one, whose collectives are not simulated here).
+        for _ in range(2):
+            device.graph2tree(shards[0], n_ids)
+        torch.cuda.synchronize()
+        ph = dict(capi.last_timings())
+        front = ["degree_sample", "front_fused", "degree_hist", "degree", "sequence", "partition",
+                 "edge_pass"]
+        best["rank0_front_ms"] = {k: round(ph[k], 3) for k in front if k in ph}
+        best["rank0_front_total_ms"] = round(sum(ph[k] for k in front if k in ph), 3)
         print(json.dumps(best), flush=True)
 
 

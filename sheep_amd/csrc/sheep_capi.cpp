@@ -453,6 +453,57 @@ struct SegPlan {
   std::vector<unsigned long long> cstart;  // host: capacity start of each bin, then the end
 };
 
+// Giant sweeps (launch_gb_sweep): after which buckets' applies the giant bitmap is completed
+// from the union-find.  The giant swallows small components bucket after bucket, and their
+// ranks miss the bitmap until a refresh meets them as the lo end of a kept pair: 102 M of the
+// 179 M pairs the RMAT-26 maps keep resolve to the giant in the refresh
+// (profiles/r05/f_sweep/refresh.jsonl).  A sweep costs a pass over the applied ranks (a find for
+// each clear bit), so it runs once the giant exists — after the bucket before the last one
+// mapped fresh (the mean degree below it crosses 1/2, fresh[]) — and then whenever the records
+// since the last sweep reach SWEEP_ALPHA x n_seq.  Tree ms at alpha 1.5 / 2.5 / 4 against none:
+// RMAT-26 14.16 / 13.95 / 14.00 vs 15.00, twitter shape 20.26 / 20.59 / 20.64 vs 21.43, RMAT-22
+// 2.35 / 2.36 / 2.44 vs 2.63, RMAT-24 5.83 / 5.88 / 5.83 vs 6.22, LJ shape within noise
+// (profiles/r05/h_sweep_alpha/).  recs(k): the records of bucket k.
+static constexpr double SWEEP_ALPHA = 2.0;
+template <typename Recs>
+static std::vector<char> sweep_plan(const std::vector<std::pair<uint32_t, uint64_t>>& bk,
+                                    Recs recs, const std::vector<char>& fresh, uint32_t n_seq) {
+  const size_t nbk = bk.size() - 1;
+  std::vector<char> sweep(nbk + 1, 0);
+  size_t kf = 0;
+  for (size_t k = 1; k < nbk && k < fresh.size(); ++k)
+    if (fresh[k]) kf = k;
+  if (kf == 0) return sweep;
+  sweep[kf - 1] = 1;
+  double acc = 0;
+  for (size_t k = kf; k + 1 < nbk; ++k) {
+    acc += (double)recs(k);
+    if (acc >= SWEEP_ALPHA * n_seq) {
+      sweep[k] = 1;
+      acc = 0;
+    }
+  }
+  return sweep;
+}
+
+// The buckets after which the mean degree 2E/B of the graph below the bucket's end crosses 1/2
+// to 1 (the giant's birth, estimated from the records): fresh[k + 1] = 1 for each (see
+// tree_from_sorted's fresh anchors).
+template <typename Recs>
+static std::vector<char> birth_window(const std::vector<std::pair<uint32_t, uint64_t>>& bk,
+                                      Recs recs) {
+  const size_t nbk = bk.size() - 1;
+  std::vector<char> fresh(nbk + 1, 0);
+  double E = 0;
+  for (size_t k = 0; k + 1 < nbk; ++k) {
+    E += (double)recs(k);
+    const double B = (double)bk[k + 1].first, d = B > 0 ? 2.0 * E / B : 0.0;
+    if (d >= 0.5) fresh[k + 1] = 1;
+    if (d >= 1.0) break;
+  }
+  return fresh;
+}
+
 static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, uint64_t m,
                              uint32_t n_seq, int lo_bit, uint32_t* d_parent, uint32_t* jump,
                              uint32_t* hcnt, bool stats, unsigned long long* ws, hipStream_t s,
@@ -540,16 +591,8 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
   // previous apply (anchored on it), not beside it.  Tree ms, default -> fresh: RMAT-26 seed 26
   // 14.8 -> 15.0, seed 5 19.7 -> 15.1, RMAT-25 seed 9 11.5 -> 9.6, RMAT-24 7.1 -> 6.2, RMAT-22
   // 3.07 -> 2.64, twitter shape 21.8 -> 21.1 (profiles/r04/ak_fresh_anchor/).
-  std::vector<char> fresh(nbk + 1, 0);
-  if (pipe) {
-    double E = 0;
-    for (size_t k = 0; k + 1 < nbk; ++k) {
-      E += (double)recs(k);
-      const double B = (double)bk[k + 1].first, d = B > 0 ? 2.0 * E / B : 0.0;
-      if (d >= 0.5) fresh[k + 1] = 1;
-      if (d >= 1.0) break;
-    }
-  }
+  std::vector<char> fresh = pipe ? birth_window(bk, recs) : std::vector<char>(nbk + 1, 0);
+  std::vector<char> sweep = sweep_plan(bk, recs, fresh, n_seq);
   auto anchor_of = [&](size_t k) -> uint32_t {
     size_t a = pipe && !fresh[k] ? k - std::min<size_t>(k, 1) : k;  // bucket whose start - 1 anchors
     return (a >= 1 && bk[a].first > 0) ? bk[a].first - 1 : INV;
@@ -623,6 +666,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
       };
       if (k + 1 < nbk && !fresh[k + 1]) next();
       apply_k(k, slot, sa);
+      if (sweep[k]) launch_gb_sweep(uf, gbits, bk[k + 1].first, gx + (slot & 1), sa);
       if (k + 1 < nbk && fresh[k + 1]) next();
     }
     if (sa != s) {  // s resumes after the last apply
@@ -1028,6 +1072,7 @@ struct Lockstep {
   uint32_t* gbits = nullptr;
   uint32_t* gx = nullptr;
   uint32_t* gsum = nullptr;  // the giant summary of the next map (launch_gb_sum, after the pick)
+  std::vector<char> sweep;   // giant sweeps after these buckets' applies (sweep_plan)
   // The maps leave their union-find misses to the apply's refresh (as the one-GPU loop does)
   // only for a one-rank group: with P ranks the refresh would repeat on every rank the finds
   // that the maps split P ways.
@@ -1260,6 +1305,8 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
 
 // The split apply for rank `rank` of P (P > 1; after ls_begin).  Its own buffers are taken from
 // the session's scratch; kept_hint: the largest P * cap the loop will apply (0: grown on demand).
+static void ls_plan_sweeps(Lockstep& L);
+
 static void ls_set_split(Lockstep& L, uint32_t rank, uint32_t P, uint64_t kept_hint) {
   if (P < 2 || rank >= P) throw ApiError(-EINVAL, "lockstep split: rank out of range or P < 2");
   Scratch& sc = *L.scp;
@@ -1278,6 +1325,19 @@ static void ls_set_split(Lockstep& L, uint32_t rank, uint32_t P, uint64_t kept_h
     HIP_CHECK(hipEventCreateWithFlags(&L.zdone[z], hipEventDisableTiming));
   }
   L.zspq = (uint32_t*)sc.get("ls_zspq", L.spq_words * 4);
+  ls_plan_sweeps(L);  // (the spacing depends on P; a no-op before ls_plan)
+}
+
+// Giant sweeps as the one-GPU loop's (sweep_plan), the birth from the global records per bucket,
+// the spacing from this rank's share of them: a sweep costs every rank a pass over the ranks,
+// and spares only the finds of its own maps (its bitmap is its own; the maps resolve their
+// misses with finds, so the exchanged pairs do not change).  At P = 8 with the one-GPU spacing:
+// maps 2.4 -> 1.8 ms per rank, applies 3.5-4.2 -> 4.4-5.0 ms (profiles/r05/i_sim/).
+static void ls_plan_sweeps(Lockstep& L) {
+  if (L.bk.size() < 2) { L.sweep.clear(); return; }
+  auto grecs = [&](size_t k) { return L.global_e[k]; };
+  auto mine = [&](size_t k) { return L.global_e[k] / std::max<uint32_t>(L.P, 1); };
+  L.sweep = sweep_plan(L.bk, mine, birth_window(L.bk, grecs), L.n_seq);
 }
 
 static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_out,
@@ -1312,6 +1372,7 @@ static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_ou
   }
   *nbk_out = (uint32_t)L.global_e.size();
   *ms_out = L.ms;
+  ls_plan_sweeps(L);
 }
 
 // d_count (nullable, device int64) receives the count without a host round trip;
@@ -1438,14 +1499,17 @@ static void ls_apply(Lockstep& L, uint32_t k, const uint64_t* d_recv, uint32_t P
     launch_ls_fold_union_label(ne, B0, B1, L.anchor(k), L.uf, L.label, d_recv, P, L.ms, cap,
                                L.bm_of(k), L.cnt_of(k), L.gbits, gx, s, anc_k,
                                L.anc ? L.anc + ((k + 1) & 1) : nullptr);
-    if (ev.second) HIP_CHECK(hipEventRecord(ev.second, s));
-    return;
+  } else {
+    if (!solo) launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
+    launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
+                    L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, L.gbits,
+                    L.gbits ? L.gx + (gslot & 1) : nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
+                    L.anc ? L.anc + ((k + 1) & 1) : nullptr);
   }
-  if (!solo) launch_ls_unpack(d_recv, P, L.ms, cap, L.bm_of(k), w0, w1, kept, L.cnt_of(k) + 3, s);
-  launch_kb_apply(L.global_e[k] > 0, B0, B1, L.anchor(k), L.uf, L.label, L.parent, L.jump, kept,
-                  L.linked, L.bm_of(k), L.spq_of(k), L.cnt_of(k), L.pipe, false, L.ws, L.gbits,
-                  L.gbits ? L.gx + (gslot & 1) : nullptr, s, L.anc ? L.anc + (k & 1) : nullptr,
-                  L.anc ? L.anc + ((k + 1) & 1) : nullptr);
+  // (after the apply, before the next pick on this stream: nothing may move the bitmap's vertex
+  // beside a sweep; the map of bucket k + 1 runs beside it)
+  if (k < L.sweep.size() && L.sweep[k] && L.gbits)
+    launch_gb_sweep(L.uf, L.gbits, B1, L.gx + (gslot & 1), s);
   if (ev.second) HIP_CHECK(hipEventRecord(ev.second, s));
 }
 

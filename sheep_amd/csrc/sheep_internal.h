@@ -264,6 +264,10 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
 // Giant summary for the next map (nothing writing gbits): bit q = ranks [64q, 64q + 64) all set
 // in gbits; (n_seq / 2048 + 1) words.
 void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStream_t s);
+// Giant sweep (sheep_kernels.hip k_gb_sweep): the giant bits of every rank v < B0lim in the
+// component of *gx, with nothing that may move *gx running beside it.
+void launch_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim, const uint32_t* gx,
+                     hipStream_t s);
 // The giant's anchor for the next map, picked on the device among ranks [0, B0lim) (the
 // component holding most of an even sample; see sheep_kernels.hip), written to *anc_out (INV
 // when B0lim = 0); gbits (nullable): the bitmap is then rebased on it (launch_gb_rebase).

@@ -3667,6 +3667,40 @@ void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStr
                      nwords, gsum);
 }
 
+// Giant sweep: every applied rank v < B0lim whose giant bit is clear and whose component is
+// that of the bitmap's reference vertex X = *gx gets its bit.  The bits are otherwise set only
+// for the ranks of a bucket that end in X's component (k_kb_label) and for the lo ends the
+// refresh finds in it, so the ranks of the small components that the giant swallows after
+// their own bucket miss the bitmap until a refresh meets them: the maps keep their records as
+// pairs for the refresh (RMAT-26: 102 M of the 179 M kept pairs resolved to the giant).  Safe
+// beside the next map (bits are only added; a root RX that another union moves below a new root
+// only loses matches) but not beside a pick that may move X (it runs on the picks' stream).
+// One wave per 64 ranks (two bitmap words): a find for each clear bit, one atomicOr per word.
+__global__ void k_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim,
+                           const uint32_t* __restrict__ gx) {
+  const uint32_t X = *gx;
+  if (X == INV || X >= B0lim) return;
+  const uint32_t RX = uf_find_ro(uf, X);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < B0lim; base += stride) {
+    const uint32_t v = base + lane;
+    bool in = false;
+    if (v < B0lim && !((gbits[v >> 5] >> (v & 31)) & 1u)) in = uf_find<true>(uf, v) == RX;
+    const uint64_t bal = __ballot(in);
+    const uint32_t half = lane < 32 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+    if ((lane & 31) == 0 && half) atomicOr(&gbits[v >> 5], half);
+  }
+}
+
+void launch_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim, const uint32_t* gx,
+                     hipStream_t s) {
+  if (B0lim == 0) return;
+  const uint32_t waves = (B0lim + 63) / 64;
+  hipLaunchKernelGGL(k_gb_sweep, dim3(std::min<uint32_t>((waves + 3) / 4, 4096)), dim3(BLOCK), 0, s,
+                     uf, gbits, B0lim, gx);
+}
+
 __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf, uint32_t anchor,
                             const uint32_t* __restrict__ gx_rd, uint32_t* gx_wr) {
   const uint32_t X = *gx_rd;
