@@ -3677,7 +3677,7 @@ void launch_gb_sum(const uint32_t* gbits, uint32_t n_seq, uint32_t* gsum, hipStr
 // only loses matches) but not beside a pick that may move X (it runs on the picks' stream).
 // One wave per 64 ranks (two bitmap words): a find for each clear bit, one atomicOr per word.
 __global__ void k_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim,
-                           const uint32_t* __restrict__ gx, int minpop) {
+                           const uint32_t* __restrict__ gx) {
   const uint32_t X = *gx;
   if (X == INV || X >= B0lim) return;
   const uint32_t RX = uf_find_ro(uf, X);
@@ -3686,8 +3686,7 @@ __global__ void k_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim,
   for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < B0lim; base += stride) {
     const uint32_t v = base + lane;
     bool in = false;
-    const uint32_t wd = v < B0lim ? gbits[v >> 5] : ~0u;
-    if (!((wd >> (v & 31)) & 1u) && __popc(wd) >= minpop) in = uf_find<true>(uf, v) == RX;
+    if (v < B0lim && !((gbits[v >> 5] >> (v & 31)) & 1u)) in = uf_find<true>(uf, v) == RX;
     const uint64_t bal = __ballot(in);
     const uint32_t half = lane < 32 ? (uint32_t)bal : (uint32_t)(bal >> 32);
     if ((lane & 31) == 0 && half) atomicOr(&gbits[v >> 5], half);
@@ -3698,9 +3697,8 @@ void launch_gb_sweep(uint32_t* uf, uint32_t* gbits, uint32_t B0lim, const uint32
                      hipStream_t s) {
   if (B0lim == 0) return;
   const uint32_t waves = (B0lim + 63) / 64;
-  static const int minpop = getenv("SHEEP_LAB_SWEEP_MINPOP") ? atoi(getenv("SHEEP_LAB_SWEEP_MINPOP")) : 0;
   hipLaunchKernelGGL(k_gb_sweep, dim3(std::min<uint32_t>((waves + 3) / 4, 4096)), dim3(BLOCK), 0, s,
-                     uf, gbits, B0lim, gx, minpop);
+                     uf, gbits, B0lim, gx);
 }
 
 __global__ void k_gb_rebase(uint32_t* gbits, uint32_t nwords, const uint32_t* uf, uint32_t anchor,
