@@ -3353,7 +3353,7 @@ static constexpr uint32_t KM_FLUSH = 65535 / KM_CHUNK;  // chunks per window flu
 // ~80 KB, so map + summary stays one block per CU and leaves ~16 KB beside it for the zipper.
 static constexpr uint32_t KM_GSUM = 16384;
 
-template <bool STATS, bool HUB = false>
+template <bool STATS, bool HUB = false, int DF = -1>
 __global__ void __launch_bounds__(KM_THREADS)
 k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, KbSegs sg,
          uint32_t B0, int gshift, uint32_t* uf, const uint32_t* __restrict__ label, uint64_t* kept,
@@ -3362,6 +3362,7 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
          const uint32_t* __restrict__ gx, int defer, const uint32_t* __restrict__ anc,
          const uint32_t* __restrict__ gsum, uint32_t gs_words, uint32_t gs_w0, uint32_t kept_cap) {
   extern __shared__ uint32_t s_gsum[];  // gs_words words of the giant summary (dynamic LDS)
+  if (DF >= 0) defer = DF;  // (compile-time for the one-GPU loop's deferred misses)
   __shared__ uint32_t wbits[KM_WIN / 32];
   __shared__ uint32_t wcnt[KM_WIN / 2];
   __shared__ uint32_t woff[KM_THREADS / 64 + 1];
@@ -3437,23 +3438,53 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       gend = (uint32_t)min((((uint64_t)(blast >> gshift)) + 1) << gshift, (uint64_t)bbase + KM_WIN);
     }
   };
-  // chunk c0's records (and its first / last hi) are loaded one chunk ahead
+  // Prefetch.  Chunk j + 1's records are loaded during chunk j.  Where the loads are issued
+  // matters: a wave's loads return in order, and a wait for a load that the compiler cannot
+  // count (a predicated one, a returning atomic) waits for everything issued before it.  With
+  // the prefetch issued right after the giant-bit loads (rounds 1-4), the classification's wait
+  // drained it within the same chunk (ISA: s_waitcnt vmcnt(0) before the bit tests).  So the
+  // records are loaded after the chunk's last uncounted wait (the classification and the
+  // out-of-window mark tests), right after the kept pairs' reservation: every record load is
+  // unpredicated (clamped to the chunk, masked later) and the reservation's result is then a
+  // counted wait; the prefetch overlaps the flush, the kept-pair stores and the next chunk's
+  // start.  A chunk's window needs no load either: in segment mode (directly binned records)
+  // a chunk lies in one bin, whose bounds are in LDS; otherwise its first and last hi are
+  // loaded a chunk ahead, before the classification.  (Past the block's last chunk the
+  // prefetch re-reads the last one: valid addresses, never used.)
   uint64_t nx[R];
-  uint32_t nh0 = 0, nbl = 0;
-  uint64_t nc0 = 0, nc1 = 0;
-  auto fetch = [&](uint32_t j) {
-    while (s_cp[si + 1] <= j) ++si;
-    nc0 = s_s0[si] + (uint64_t)(j - s_cp[si]) * KM_CHUNK;
-    nc1 = min(nc0 + (uint64_t)KM_CHUNK, s_s0[si] + s_len[si]);
+  auto bounds_of = [&](uint32_t j, uint64_t& b0, uint64_t& b1, uint32_t& sj) {
+    while (s_cp[si + 1] <= j) ++si;  // (j only grows over the calls)
+    b0 = s_s0[si] + (uint64_t)(j - s_cp[si]) * KM_CHUNK;
+    b1 = min(b0 + (uint64_t)KM_CHUNK, s_s0[si] + s_len[si]);
+    sj = si;
+  };
+  auto fetch = [&](uint64_t b0, uint64_t b1) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint64_t idx = nc0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
-      nx[r] = idx < nc1 ? __builtin_nontemporal_load(&items[idx]) : 0ull;  // streamed once
+      const uint64_t idx = b0 + (uint64_t)r * KM_THREADS + (uint64_t)w * 64 + lane;
+      nx[r] = __builtin_nontemporal_load(&items[min(idx, b1 - 1)]);  // streamed once
     }
-    nh0 = (uint32_t)(items[nc0] >> 32);
-    nbl = (uint32_t)(items[nc1 - 1] >> 32);
   };
-  if (j0 < j1) fetch(j0);
+  const bool segw = sg.start != nullptr && bins != nullptr;  // windows from the segments' bins
+  auto seg_window = [&](uint32_t sj, uint32_t& bbase, uint32_t& gend) {
+    const uint32_t b = sg.i0 + sj;
+    bbase = sbins[b] & ~31u;
+    gend = (uint32_t)min((uint64_t)sbins[min(b + 1, nb - 1)], (uint64_t)bbase + KM_WIN);
+    if (gend <= bbase) gend = bbase + 1;
+  };
+  uint64_t nc0 = 0, nc1 = 0, pc0 = 0, pc1 = 0;  // chunk j's and chunk j + 1's records
+  uint32_t ns = 0, ps = 0;                      // ... their segments
+  uint32_t nh0 = 0, nbl = 0;                    // (not segment mode) chunk j's first, last hi
+  if (j0 < j1) {
+    bounds_of(j0, nc0, nc1, ns);
+    fetch(nc0, nc1);
+    if (!segw) {
+      nh0 = (uint32_t)(items[nc0] >> 32);
+      nbl = (uint32_t)(items[nc1 - 1] >> 32);
+    }
+    if (j0 + 1 < j1) bounds_of(j0 + 1, pc0, pc1, ps);
+    else { pc0 = nc0; pc1 = nc1; ps = ns; }
+  }
   uint32_t since_flush = 0;
   for (uint32_t j = j0; j < j1; ++j) {
     const uint64_t c0 = nc0, c1 = nc1;
@@ -3467,7 +3498,13 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     }
     // the chunk's records lie in [group (or bin) of its first record, that of its last)
     uint32_t bbase, gend;
-    window(nh0, nbl, bbase, gend);
+    if (segw) seg_window(ns, bbase, gend);
+    else window(nh0, nbl, bbase, gend);
+    uint32_t qh0 = 0, qbl = 0;  // (not segment mode) chunk j + 1's first and last hi
+    if (!segw) {
+      qh0 = (uint32_t)(items[pc0] >> 32);
+      qbl = (uint32_t)(items[pc1 - 1] >> 32);
+    }
     const uint32_t span = gend - bbase;  // ranks of the window that can hold records
     // Narrow windows (hub bins: few ranks, many records each) keep RF u32 copies of each
     // rank's count, lane l adding to copy l % RF: a hub's lanes in one wave then hit RF
@@ -3487,7 +3524,6 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
       gw[r] = full ? ~0u : (t_ ? gbits[a >> 5] : 0u);
     }
     const bool more = j + 1 < j1;
-    if (more) fetch(j + 1);  // issued after the bitmap loads
     uint32_t giant = 0, miss = 0, x[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -3570,10 +3606,29 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
     bool flush = !more || (++since_flush >= KM_FLUSH && RF == 1);
     if (!flush) {
       uint32_t nbase, nend;
-      window(nh0, nbl, nbase, nend);
+      if (segw) seg_window(ps, nbase, nend);
+      else window(qh0, qbl, nbase, nend);
       flush = nbase != bbase || nend != gend;
     }
     block_sync();
+    // compaction: one reservation per chunk for the kept pairs of all its waves (issued here,
+    // before the prefetch, so that its result is a counted wait).  Guard: a chunk keeps at most
+    // its records and the host sizes kept for the bucket's records, so a reservation past
+    // kept_cap means corrupt counts; it raises the fault word (-EIO), nothing is written past
+    // kept_cap, and n_kept is clamped to it (every later reservation is past it too and clamps
+    // again), so the refresh and the zipper read only written slots.
+    uint32_t kbase = 0, krun = 0;
+    if (t == 0) {
+      for (int i = 0; i < KM_THREADS / 64; ++i) { uint32_t v = woff[i]; woff[i] = krun; krun += v; }
+      // (an address the compiler cannot prove uniform — mbcnt of an empty mask is 0 — keeps
+      // the atomic optimizer from broadcasting the result with readfirstlane right away, which
+      // waits for it, and for the prefetch behind it)
+      if (krun) kbase = atomicAdd(n_kept + __builtin_amdgcn_mbcnt_lo(0u, 0u), krun);
+    }
+    // the prefetch: chunk j + 1's records (chunk j's again past the block's last)
+    fetch(pc0, pc1);
+    nc0 = pc0; nc1 = pc1; ns = ps; nh0 = qh0; nbl = qbl;
+    if (j + 2 < j1) bounds_of(j + 2, pc0, pc1, ps);
     if (flush) {
       since_flush = 0;
       for (uint32_t i = t; i < (span + 31) / 32; i += KM_THREADS) {
@@ -3603,20 +3658,12 @@ k_kb_map(const uint64_t* __restrict__ items, uint64_t e_begin, uint64_t e_end, K
         }
       }
     }
-    // compaction: one reservation per chunk for the kept pairs of all its waves.  Guard: a
-    // chunk keeps at most its records and the host sizes kept for the bucket's records, so a
-    // reservation past kept_cap means corrupt counts; it raises the fault word (-EIO), nothing
-    // is written past kept_cap, and n_kept is clamped to it (every later reservation is past it
-    // too and clamps again), so the refresh and the zipper read only written slots.
     if (t == 0) {
-      uint32_t run = 0;
-      for (int i = 0; i < KM_THREADS / 64; ++i) { uint32_t v = woff[i]; woff[i] = run; run += v; }
-      const uint32_t base = run ? atomicAdd(n_kept, run) : 0u;
-      if (run && (uint64_t)base + run > kept_cap) {
+      if (krun && (uint64_t)kbase + krun > kept_cap) {
         raise_fault(FAULT_KEPT);
         atomicMin(n_kept, kept_cap);
       }
-      woff[KM_THREADS / 64] = base;
+      woff[KM_THREADS / 64] = kbase;
     }
     block_sync();
     uint32_t pos = woff[KM_THREADS / 64] + woff[w];
@@ -4080,7 +4127,8 @@ void launch_kb_map(const uint64_t* items, uint64_t e_begin, uint64_t e_end, uint
   unsigned grid = (unsigned)std::min<uint64_t>(chunks, device_cus());
   const bool hub = e_end - e_begin >= (1ull << 25);
   auto mk = stats ? (hub ? k_kb_map<true, true> : k_kb_map<true, false>)
-                  : (hub ? k_kb_map<false, true> : k_kb_map<false, false>);
+          : defer == 1 ? (hub ? k_kb_map<false, true, 1> : k_kb_map<false, false, 1>)
+                       : (hub ? k_kb_map<false, true> : k_kb_map<false, false>);
   // the giant summary of the highest KM_GSUM words of ranks below B0 (the lo ends of most
   // records: a vertex is the lo end of its edges to higher-degree vertices) in dynamic LDS
   const uint32_t w_end = (B0 + 2047) / 2048;
