@@ -44,7 +44,7 @@ static const KnobDef kKnobs[] = {
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
-    {"kb_merge", &Knobs::kb_merge},
+    {"kb_merge", &Knobs::kb_merge},       {"lab", &Knobs::lab},
 };
 
 static Knobs g_knobs;

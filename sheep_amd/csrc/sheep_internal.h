@@ -57,6 +57,7 @@ struct Knobs {
   int kb_merge = 35;     // SHEEP_KB_MERGE: merge adjacent kb buckets while together they hold at
                          //   most kb_merge / 10000 of the records (0: off;
                          //   the lockstep loop: 20 unless off)
+  int lab = 0;           // SHEEP_LAB: bit mask of kernel variants under A/B (lab only)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };

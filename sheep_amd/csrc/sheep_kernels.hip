@@ -729,6 +729,14 @@ k_degb_scatter_cap(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int
 // Tile: FF_NT x FF_IT records.  LDS: the tile staged twice 64 KB (x; digit << 16 | y_lo), the x
 // endpoints restaged into the first half, and the run tables of both sorts.
 static constexpr int FF_NT = 1024, FF_IT = 16;
+// Persistent: gridDim blocks (one per CU) walk the tiles blockIdx.x, + gridDim.x, ...  The x runs are
+// staged and written first, then the y runs staged; the next tile's records are loaded right
+// after that (the last use of this tile's records in registers) so that their HBM latency
+// overlaps the y write-out instead of opening the next tile with an idle CU (one block per CU:
+// the two 64 KB stages fill the LDS).  No uncounted wait lies between the loads and their use:
+// the y write-out holds stores only, and the barriers wait for LDS operations alone.  (RMAT-26
+// 8.04 -> 7.79 ms on one box, profiles/r05/q_fused_pipe_et/; the capacity check of the y runs
+// moved from a global load per record of the write-out to an LDS table, yfit.)
 __global__ void __launch_bounds__(FF_NT)
 k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
               uint32_t NB, uint32_t* __restrict__ oa, uint16_t* __restrict__ ob,
@@ -741,18 +749,29 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
   __shared__ uint32_t sa[TILE], sb[TILE];
   __shared__ uint32_t ty[DEGB_NB + 1], tx[DEGB_NB + 1], hxd[PD_X], wsum[2 * (FF_NT / 64)];
   __shared__ unsigned long long gy[DEGB_NB], gx[DEGB_NB];
+  __shared__ uint32_t yfit[DEGB_NB];  // the part of a y run that fits its capacity region
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t lmask = (1u << SH) - 1u;
+  const uint64_t ntiles = (m + TILE - 1) / TILE;
+  uint2 e[FF_IT];
+  auto load = [&](uint64_t tile) {  // unpredicated (clamped to the tile's last record)
+    const uint2* p = uv + tile * TILE;
+    const uint32_t last = (uint32_t)min((uint64_t)TILE, m - tile * TILE) - 1u;
+    uint32_t o = t;
+    asm volatile("" : "+v"(o));  // (keeps the 16 offsets from being hoisted out of the tile loop)
+#pragma unroll
+    for (int k = 0; k < FF_IT; ++k) e[k] = ld_rec_nt(p + min((uint32_t)k * FF_NT + o, last));
+  };
+  uint64_t tile = blockIdx.x;
+  load(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
   for (uint32_t i = t; i < DEGB_NB; i += FF_NT) { ty[i] = 0; tx[i] = 0; }
   for (uint32_t i = t; i < PD_X; i += FF_NT) hxd[i] = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint64_t base = tile * TILE;
   const uint32_t cn = (uint32_t)min((uint64_t)TILE, m - base);
-  uint2 e[FF_IT];
-#pragma unroll
-  for (int k = 0; k < FF_IT; ++k) {
-    const uint32_t i = (uint32_t)k * FF_NT + t;
-    e[k] = i < cn ? ld_rec_nt(uv + base + i) : make_uint2(INV, INV);
-  }
+  // the records have arrived (one wait here: the compiler then counts none of the loads as
+  // pending behind the x write-out's stores, which a later wait would otherwise drain)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   block_sync();
   uint32_t ly[FF_IT], lx[FF_IT];  // rank within the tile's y run / x run (INV: none)
 #pragma unroll
@@ -760,8 +779,9 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     ly[k] = INV;
     lx[k] = INV;
     const uint2 r = e[k];
+    if ((uint32_t)k * FF_NT + t >= cn) continue;
     if (r.x >= n_ids || r.y >= n_ids) {
-      if ((uint32_t)k * FF_NT + t < cn) atomicOr(err, ERR_RANGE);
+      atomicOr(err, ERR_RANGE);
       continue;
     }
     ly[k] = atomicAdd(&ty[r.y >> SH], 1u);
@@ -782,10 +802,14 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     if (lane == 63) { wsum[w] = i1; wsum[FF_NT / 64 + w] = i2; }
     unsigned long long g1 = 0, g2 = ~0ull;
     if ((uint32_t)t < NB) {
+      uint32_t fit = 0;
       if (c1) {
         g1 = atomicAdd(&ycur[t], (unsigned long long)c1);
-        if (g1 + c1 > ycap[t]) atomicOr(ovf_y, 1u);
+        const unsigned long long cap = ycap[t];
+        fit = g1 + c1 <= cap ? c1 : g1 < cap ? (uint32_t)(cap - g1) : 0u;
+        if (fit < c1) atomicOr(ovf_y, 1u);
       }
+      yfit[t] = fit;
       if (c2) {
         g2 = atomicAdd(&bcur[t], (unsigned long long)c2);
         if (g2 + c2 > bcap[t]) {
@@ -812,24 +836,6 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
   block_sync();
 #pragma unroll
   for (int k = 0; k < FF_IT; ++k)
-    if (ly[k] != INV) {
-      const uint32_t d = e[k].y >> SH, j = ty[d] + ly[k];
-      sa[j] = e[k].x;
-      sb[j] = (d << 16) | (e[k].y & lmask);
-    }
-  block_sync();
-  const uint32_t ny = ty[NB];
-  for (uint32_t j = t; j < ny; j += FF_NT) {  // flat: every lane busy
-    const uint32_t v = sb[j], d = v >> 16;
-    const unsigned long long pos = gy[d] + (j - ty[d]);
-    if (pos < ycap[d]) {
-      oa[pos] = sa[j];
-      ob[pos] = (uint16_t)(v & 0xFFFFu);
-    }
-  }
-  block_sync();
-#pragma unroll
-  for (int k = 0; k < FF_IT; ++k)
     if (lx[k] != INV) {
       const uint32_t b = e[k].x >> SH;
       sa[tx[b] + lx[k]] = (b << 16) | (e[k].x & lmask);
@@ -840,6 +846,28 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     const uint32_t v = sa[j], b = v >> 16;
     const unsigned long long g = gx[b];
     if (g != ~0ull) ep[g + (j - tx[b])] = (uint16_t)(v & 0xFFFFu);
+  }
+  block_sync();
+#pragma unroll
+  for (int k = 0; k < FF_IT; ++k)
+    if (ly[k] != INV) {
+      const uint32_t d = e[k].y >> SH, j = ty[d] + ly[k];
+      sa[j] = e[k].x;
+      sb[j] = (d << 16) | (e[k].y & lmask);
+    }
+  load(min(tile + gridDim.x, ntiles - 1));  // (past the last tile: re-read, unused)
+  block_sync();
+  const uint32_t ny = ty[NB];
+  for (uint32_t j = t; j < ny; j += FF_NT) {  // flat: every lane busy
+    const uint32_t v = sb[j], d = v >> 16;
+    const uint32_t i = j - ty[d];
+    if (i < yfit[d]) {
+      const unsigned long long pos = gy[d] + i;
+      oa[pos] = sa[j];
+      ob[pos] = (uint16_t)(v & 0xFFFFu);
+    }
+  }
+  block_sync();  // (the tables and stages are reset / rewritten by the next tile)
   }
 }
 
@@ -1335,7 +1363,8 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   uint32_t* oa = (uint32_t*)mid;
   uint16_t* ob = (uint16_t*)(oa + mid_slots);
   const unsigned nt = (unsigned)((m + FF_NT * FF_IT - 1) / (FF_NT * FF_IT));
-  hipLaunchKernelGGL(k_front_fused, dim3(nt), dim3(FF_NT), 0, s, (const uint2*)uv, m, n_ids,
+  hipLaunchKernelGGL(k_front_fused, dim3(std::min(nt, device_cus())), dim3(FF_NT), 0, s,
+                     (const uint2*)uv, m, n_ids,
                      file_mode, SH, NB, oa, ob, ycur, (const unsigned long long*)ycap, bcur,
                      (const unsigned long long*)bcap, ep, selfc, ovf_y, ovf_x, err,
                      part_ws + PW_X, part_shift(n_ids, PD_X),
@@ -2421,6 +2450,29 @@ __device__ __forceinline__ void search512(const uint32_t* tb, const uint32_t* v,
   for (int k = 0; k < N; ++k) idx[k] = lo[k];
 }
 
+// The same search over the table in Eytzinger order (et[n] = tb[probe of node n], n = 1..511;
+// et_of gives the entry): the nodes probed at one depth are contiguous, so the lanes of a wave
+// read distinct banks, where the sorted layout's probes at one depth lie a power of two apart
+// (one bank) — k_edge_bin's bank-conflict fraction was 0.69 (round 4 counters); RMAT-26 edge
+// pass 7.50 -> 6.83 ms (profiles/r05/q_fused_pipe_et/).
+__device__ __forceinline__ uint32_t et_index(uint32_t n) {  // node n >= 1 -> sorted index
+  const uint32_t d = 31u - __builtin_clz(n);
+  return ((n - (1u << d)) << (9u - d)) + (256u >> d);
+}
+template <int N>
+__device__ __forceinline__ void search512_et(const uint32_t* et, const uint32_t* v, uint32_t* idx) {
+  uint32_t n[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) n[k] = 1;
+#pragma unroll
+  for (int d = 0; d < 9; ++d) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) n[k] = 2 * n[k] + (et[n[k]] <= v[k] ? 1u : 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) idx[k] = n[k] - 512u;
+}
+
 // IN6 (with PRE): the records are k_part<1>'s packed output; x's digit bits come from the
 // x-digit region starts xst (shx: the digit shift).
 // PK (every rank < 2^26): a staged slot holds bin << 52 | hi << 26 | lo, so the write-out reads
@@ -2443,7 +2495,8 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
   const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
   if (t < 512) {
     hist[t] = 0;
-    sb[t] = (uint32_t)t < nb ? bins[t] : INV;  // padded: search512
+    const uint32_t i = t ? et_index(t) : 0u;  // Eytzinger order (search512_et; sb[0] unused)
+    sb[t] = i < nb ? bins[i] : INV;            // padded
   }
   uint2 e[IT];
   uint32_t rx[IT], ry[IT];
@@ -2506,7 +2559,7 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
     item[k] = ((uint64_t)hi << 32) | lo;
     hiv[k] = hi == INV ? 0u : hi;  // searched anyway (no divergence), not stored
   }
-  search512<IT>(sb, hiv, pk);
+  search512_et<IT>(sb, hiv, pk);
 #pragma unroll
   for (int k = 0; k < IT; ++k)
     pk[k] = (uint32_t)(item[k] >> 32) != INV ? (pk[k] << 16) | atomicAdd(&hist[pk[k]], 1u) : ~0u;
