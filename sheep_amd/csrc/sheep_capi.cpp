@@ -152,6 +152,8 @@ static void ctx_teardown(Ctx& c) {
   for (auto& e : c.kb_ev) (void)hipEventDestroy(e);
   for (auto& e : c.part_ev) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c.bins_ev);
+  for (hipEvent_t e : c.ev_pool) (void)hipEventDestroy(e);
+  c.ev_pool.clear();
   (void)hipHostFree(c.h_bstart);
   if (c.h_chunks) (void)hipHostFree(c.h_chunks);
   (void)hipFree(c.d_err);
@@ -186,17 +188,29 @@ static hipStream_t pick(Ctx& c, void* stream) {
   return (hipStream_t)stream;
 }
 
-// Phase timing with HIP events on the working stream.
+// Phase timing with HIP events on the working stream.  The events come from the context's
+// pool and go back to it (creating and destroying ~120 events per graph2tree call cost about
+// 0.4 ms of host time, the destruction after the GPU had finished).
 struct Timer {
   hipStream_t s;
+  std::vector<hipEvent_t>* pool;
   std::vector<std::pair<const char*, hipEvent_t>> ev;
-  explicit Timer(hipStream_t st) : s(st) { mark("start"); }
+  explicit Timer(hipStream_t st) : s(st), pool(&ctx().ev_pool) { mark("start"); }
+  hipEvent_t take() {
+    if (pool->empty()) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      return e;
+    }
+    hipEvent_t e = pool->back();
+    pool->pop_back();
+    return e;
+  }
   // host-side durations (ms), reported after the device phases
   std::vector<std::pair<const char*, double>> host;
   void host_ms(const char* name, double ms) { host.emplace_back(name, ms); }
   void mark(const char* name) {
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreate(&e));
+    hipEvent_t e = take();
     HIP_CHECK(hipEventRecord(e, s));
     ev.emplace_back(name, e);
   }
@@ -204,9 +218,7 @@ struct Timer {
   // in finish(): "<name>" = total ms, "<name>#" = launches.
   std::vector<std::tuple<const char*, hipEvent_t, hipEvent_t>> spans;
   size_t span_begin(const char* name, hipStream_t st) {
-    hipEvent_t a, b;
-    HIP_CHECK(hipEventCreate(&a));
-    HIP_CHECK(hipEventCreate(&b));
+    hipEvent_t a = take(), b = take();
     HIP_CHECK(hipEventRecord(a, st));
     spans.emplace_back(name, a, b);
     return spans.size() - 1;
@@ -237,11 +249,11 @@ struct Timer {
     }
     for (auto& x : host) c.timings.push_back(x);
   }
-  ~Timer() {
-    for (auto& e : ev) (void)hipEventDestroy(e.second);
+  ~Timer() {  // (a recorded event may be re-recorded: the pool holds them for the next call)
+    for (auto& e : ev) pool->push_back(e.second);
     for (auto& sp : spans) {
-      (void)hipEventDestroy(std::get<1>(sp));
-      (void)hipEventDestroy(std::get<2>(sp));
+      pool->push_back(std::get<1>(sp));
+      pool->push_back(std::get<2>(sp));
     }
   }
 };
@@ -392,16 +404,20 @@ static bool use_part(uint64_t m) {
 // stats_ready: the degree pass already wrote max degree / zero-degree count to "stats".
 // nsd (nullable, n_ids words): rank-ordered non-self-loop degrees (k_unpack_seq) for these
 // same records' selfc / mode.
+// stats_host: ... and they are already in c.h_pinned[0..1] (read back with another word).
 static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint32_t* d_seq,
                              uint32_t* d_rank, hipStream_t s, bool stats_ready = false,
                              uint32_t* nsd = nullptr, const uint32_t* selfc = nullptr,
-                             int mode = 0) {
+                             int mode = 0, bool stats_host = false) {
   if (n_ids == 0) return 0;
   uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
   if (!stats_ready) launch_deg_stats(d_deg, n_ids, stats, s);
-  HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 8, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  uint32_t maxdeg = c.h_pinned[0], zeros = c.h_pinned[1];
+  if (!stats_host) {
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 12, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+  // max degree, zero-degree ids, ids of degree >= seqc_threshold() (the radix-sorted tail)
+  const uint32_t maxdeg = c.h_pinned[0], zeros = c.h_pinned[1], n_big = c.h_pinned[2];
   uint32_t n_seq = n_ids - zeros;
   if (n_seq == 0) {
     if (d_rank) launch_fill(d_rank, INV, n_ids, s);
@@ -412,10 +428,10 @@ static uint32_t sequence_dev(Ctx& c, const uint32_t* d_deg, uint32_t n_ids, uint
   uint64_t* big = (uint64_t*)c.scratch.get("seq_items", (size_t)n_seq * 8);
   const uint32_t* sc = nsd ? selfc : nullptr;  // the self-loop records off nsd in place
   const uint32_t* first = launch_seqc_place(d_deg, n_ids, d_seq, d_rank, nsd, big, qtmp, s, sc, mode);
+  (void)first;  // (its first position is n_seq - n_big: no readback)
   if (maxdeg >= seqc_threshold()) {
-    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 2, first, 4, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    const uint32_t base = c.h_pinned[2], n_big = n_seq - base;
+    if (n_big == 0 || n_big > n_seq) throw ApiError(-EIO, "sequence: degree stats disagree");
+    const uint32_t base = n_seq - n_big;
     uint64_t* big_b = (uint64_t*)c.scratch.get("seq_items_b", (size_t)n_big * 8);
     uint32_t* tmp = (uint32_t*)c.scratch.get("rsort_tmp", rsort_tmp_words(n_big) * 4);
     uint64_t* sorted = radix_sort_u64(big, big_b, big, n_big, 0, bits_for(maxdeg), tmp, s);
@@ -2069,6 +2085,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
   uint32_t* ovf_part = c.d_err + 3;
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
   bool yh = false;
+  bool stats_host = false;  // the degree stats already read back (sequence_dev skips its readback)
   if (ffused) {
     HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words
     uint32_t* tmp = (uint32_t*)c.scratch.get("degs_tmp", degs_tmp_words(m, n_ids) * 4);
@@ -2079,12 +2096,19 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
                        [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
     tm.mark("degree_hist");
     HIP_CHECK(hipEventRecord(c.part_ev[1], s));
-    // the degrees are complete unless an x bucket outgrew its region
-    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 4, hipMemcpyDeviceToHost, s));
+    // One readback: the error word and both overflow words (d_err[0..3]) with the degree stats.
+    // The degrees are complete unless an x bucket outgrew its region; an id out of range leaves
+    // the pass's record array short, which is reported here, before anything reads it (the
+    // check_err the sequence would otherwise need).
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, c.d_err, 16, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 12, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (c.h_pinned[4]) {
+    if (c.h_pinned[4] & ERR_RANGE) check_err(c, s);  // (throws -ERANGE, resetting the word)
+    stats_host = true;
+    if (c.h_pinned[6]) {
       degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, false, nullptr, stats);
       tm.mark("degree_exact");
+      stats_host = false;  // (the exact pass rewrote them)
     }
   } else if (sampled) {
     HIP_CHECK(hipMemsetAsync(ovf_deg, 0, 8, s));  // both overflow words
@@ -2126,10 +2150,12 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     HIP_CHECK(hipEventRecord(c.part_ev[1], c.side));
   }
   uint32_t* nsd = (uint32_t*)c.scratch.get("nsd", (size_t)std::max<uint32_t>(n_ids, 1) * 4);
-  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true, nsd, selfc, degree_mode);
+  uint32_t n_seq = sequence_dev(c, deg, n_ids, d_seq, rank, s, true, nsd, selfc, degree_mode,
+                                stats_host);
   // an id out of range leaves the fused pass's record array short: report it before the
-  // partition passes read the array (the stream is idle here: sequence_dev synchronised it)
-  if (fused) check_err(c, s);
+  // partition passes read the array (the stream is idle here: sequence_dev synchronised it;
+  // the sampled fused pass read its error word above, unless the exact degree pass ran since)
+  if (fused && !stats_host) check_err(c, s);
   tm.mark("sequence");
   DegInfo di;
   di.nsd = nsd;

@@ -78,6 +78,7 @@ struct Ctx {
   uint32_t* h_pinned = nullptr;  // pinned host words for small readbacks
   std::vector<std::pair<const char*, double>> timings;
   std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
+  std::vector<hipEvent_t> ev_pool;     // timing events of finished calls (Timer), reused
   int ls_live = 0;                     // live lockstep sessions (sheep_ls_*) on this device
   struct Comm* comm = nullptr;         // this rank's communicator (sheep_comm_init), if any
   // host record ranges declared immutable (sheep_records_register / sheep_records_load_dat)

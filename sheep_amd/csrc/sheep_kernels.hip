@@ -157,41 +157,52 @@ void launch_pst_from_degree(const uint64_t* sorted, uint64_t m, const uint32_t* 
                      selfc, file_mode ? 2u : 1u, (const uint32_t*)start, (const uint32_t*)end, pst);
 }
 
-// stats[0] = max degree, stats[1] = number of zero-degree ids.
+// stats[0] = max degree, stats[1] = number of zero-degree ids, stats[2] = number of ids of
+// degree >= SEQ_BIG (the sequence's radix-sorted tail: its size is then known with the other
+// two, and the sequence needs no readback of where the tail starts).
+static constexpr uint32_t SEQ_BIG = 1024;
 __device__ __forceinline__ void block_sync();
 // Max degree and zero-degree count: 16-B loads when deg is 16-B aligned (V4; else one word per
 // load), one pair of atomics per workgroup.
 template <bool V4>
 __global__ void k_deg_stats(const uint32_t* __restrict__ deg, uint32_t n, uint32_t* stats) {
-  __shared__ uint32_t smx[BLOCK / 64], szr[BLOCK / 64];
-  uint32_t mx = 0, zeros = 0;
+  __shared__ uint32_t smx[BLOCK / 64], szr[BLOCK / 64], sbg[BLOCK / 64];
+  uint32_t mx = 0, zeros = 0, big = 0;
   const uint32_t n4 = V4 ? n / 4 : 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const uint4 q = ((const uint4*)deg)[i];
     mx = max(max(mx, max(q.x, q.y)), max(q.z, q.w));
     zeros += (q.x == 0) + (q.y == 0) + (q.z == 0) + (q.w == 0);
+    big += (q.x >= SEQ_BIG) + (q.y >= SEQ_BIG) + (q.z >= SEQ_BIG) + (q.w >= SEQ_BIG);
   }
   for (uint32_t i = 4 * n4 + blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += gridDim.x * blockDim.x) {
     const uint32_t d = deg[i];
     mx = max(mx, d);
     zeros += d == 0;
+    big += d >= SEQ_BIG;
   }
   for (int o = 32; o > 0; o >>= 1) {
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     zeros += (uint32_t)__shfl_xor((int)zeros, o);
+    big += (uint32_t)__shfl_xor((int)big, o);
   }
-  if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = mx; szr[threadIdx.x >> 6] = zeros; }
+  if ((threadIdx.x & 63) == 0) {
+    smx[threadIdx.x >> 6] = mx;
+    szr[threadIdx.x >> 6] = zeros;
+    sbg[threadIdx.x >> 6] = big;
+  }
   block_sync();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < BLOCK / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; }
+    for (int i = 1; i < BLOCK / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; big += sbg[i]; }
     if (mx) atomicMax(&stats[0], mx);
     if (zeros) atomicAdd(&stats[1], zeros);
+    if (big) atomicAdd(&stats[2], big);
   }
 }
 
 void launch_deg_stats(const uint32_t* deg, uint32_t n, uint32_t* stats, hipStream_t s) {
-  (void)hipMemsetAsync(stats, 0, 8, s);
+  (void)hipMemsetAsync(stats, 0, 12, s);
   if (n == 0) return;
   const bool v4 = ((uintptr_t)deg & 15) == 0;
   hipLaunchKernelGGL(v4 ? k_deg_stats<true> : k_deg_stats<false>,
@@ -336,18 +347,25 @@ __device__ __forceinline__ uint2 ld_rec_nt(const uint2* p) {
 }
 // k_deg_stats folded into the histogram kernels: the block's max degree and zero-degree ids,
 // two global atomics per block (called by every thread of a DEGB_THREADS block).
-__device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, uint32_t zeros) {
-  __shared__ uint32_t smx[DEGB_THREADS / 64], szr[DEGB_THREADS / 64];
+__device__ __forceinline__ void deg_stats_flush(uint32_t* stats, uint32_t mx, uint32_t zeros,
+                                                uint32_t big) {
+  __shared__ uint32_t smx[DEGB_THREADS / 64], szr[DEGB_THREADS / 64], sbg[DEGB_THREADS / 64];
   for (int o = 32; o > 0; o >>= 1) {
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     zeros += (uint32_t)__shfl_xor((int)zeros, o);
+    big += (uint32_t)__shfl_xor((int)big, o);
   }
-  if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = mx; szr[threadIdx.x >> 6] = zeros; }
+  if ((threadIdx.x & 63) == 0) {
+    smx[threadIdx.x >> 6] = mx;
+    szr[threadIdx.x >> 6] = zeros;
+    sbg[threadIdx.x >> 6] = big;
+  }
   block_sync();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < DEGB_THREADS / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; }
+    for (int i = 1; i < DEGB_THREADS / 64; ++i) { mx = max(mx, smx[i]); zeros += szr[i]; big += sbg[i]; }
     if (mx) atomicMax(&stats[0], mx);
     if (zeros) atomicAdd(&stats[1], zeros);
+    if (big) atomicAdd(&stats[2], big);
   }
 }
 // Tile-major count matrices and their scan (defined with the hi bins below).
@@ -957,15 +975,16 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
   }  // segments
   block_sync();
   uint64_t g0 = ((uint64_t)b << SH) + (uint64_t)h * span;
-  uint32_t mx = 0, zeros = 0;
+  uint32_t mx = 0, zeros = 0, big = 0;
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x)
     if (g0 + i < n_ids) {
       const uint32_t d = cnt[i];
       deg[g0 + i] = d;
       mx = max(mx, d);
       zeros += d == 0;
+      big += d >= SEQ_BIG;
     }
-  if (stats) deg_stats_flush(stats, mx, zeros);
+  if (stats) deg_stats_flush(stats, mx, zeros, big);
 }
 
 // Buckets of 65536 ids (n_ids > 2^25): one workgroup per bucket reads the bucket's run ONCE
@@ -1063,7 +1082,7 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
   }
   }  // segments
   const uint64_t base = (uint64_t)b << 16;
-  uint32_t mx = 0, zeros = 0;
+  uint32_t mx = 0, zeros = 0, big = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     const uint64_t id = base + (uint64_t)k * DEGB_THREADS + threadIdx.x;
@@ -1071,9 +1090,10 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
       deg[id] = acc[k];
       mx = max(mx, acc[k]);
       zeros += acc[k] == 0;
+      big += acc[k] >= SEQ_BIG;
     }
   }
-  if (stats) deg_stats_flush(stats, mx, zeros);
+  if (stats) deg_stats_flush(stats, mx, zeros, big);
 }
 
 // k_degb_hist16 in slices (the fused front pass's histogram): bucket b's entries, x endpoints
@@ -1084,6 +1104,31 @@ k_degb_hist16(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offs
 // caller zeroed.  One workgroup per bucket left the step waiting on the buckets of the hub ids
 // and on the last round of buckets over the CUs.  Counting as k_degb_hist16 (u16 halves of
 // 32768 LDS words, segments of at most 65535 entries, u32 totals in registers).
+// Slices of bucket t (thread t of a 1024-thread block, t < NB) and the first slice's block
+// index (an exclusive scan over the buckets; wsum: DEGB_THREADS / 64 words of LDS).
+__device__ __forceinline__ void hist16s_slices(const unsigned long long* __restrict__ xs,
+                                               const unsigned long long* __restrict__ xf,
+                                               const unsigned long long* __restrict__ ys,
+                                               const unsigned long long* __restrict__ yf,
+                                               uint32_t NB, uint64_t CH, uint32_t* wsum,
+                                               uint32_t& ns, uint32_t& p0) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  ns = 0;
+  if ((uint32_t)t < NB) {
+    const uint64_t nx = min(xs[t + 1], xf[t]) - min(xs[t], min(xs[t + 1], xf[t]));
+    const uint64_t ny = min(ys[t + 1], yf[t]) - min(ys[t], min(ys[t + 1], yf[t]));
+    ns = (uint32_t)max((uint64_t)1, (nx + ny + CH - 1) / CH);
+  }
+  const uint32_t incl = wave_incl_scan(ns);
+  if (lane == 63) wsum[w] = incl;
+  block_sync();
+  uint32_t add = 0;
+  for (int i = 0; i < w; ++i) add += wsum[i];
+  p0 = add + incl - ns;
+}
+
+// (Partial counts of a split bucket's later slices stored to a buffer and added by a second
+// kernel, instead of the atomics here, measured no faster: RMAT-26 hist 2.00 -> 2.04 ms.)
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __restrict__ xs,
                const unsigned long long* __restrict__ xf, const uint16_t* __restrict__ ey,
@@ -1091,22 +1136,11 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
                uint32_t NB, uint32_t n_ids, uint64_t CH, uint32_t* __restrict__ deg) {
   __shared__ uint32_t pk[32768];
   __shared__ uint32_t wsum[DEGB_THREADS / 64], s_b, s_s, s_n;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   // slice table: thread t = bucket t
-  uint64_t nx = 0, ny = 0;
-  uint32_t ns = 0;
-  if ((uint32_t)t < NB) {
-    nx = min(xs[t + 1], xf[t]) - min(xs[t], min(xs[t + 1], xf[t]));
-    ny = min(ys[t + 1], yf[t]) - min(ys[t], min(ys[t + 1], yf[t]));
-    ns = (uint32_t)max((uint64_t)1, (nx + ny + CH - 1) / CH);
-  }
-  const uint32_t incl = wave_incl_scan(ns);
-  if (lane == 63) wsum[w] = incl;
   if (t == 0) s_b = INV;
-  block_sync();
-  uint32_t add = 0;
-  for (int i = 0; i < w; ++i) add += wsum[i];
-  const uint32_t p0 = add + incl - ns;
+  uint32_t ns, p0;
+  hist16s_slices(xs, xf, ys, yf, NB, CH, wsum, ns, p0);
   if ((uint32_t)t < NB && blockIdx.x >= p0 && blockIdx.x < p0 + ns) {
     s_b = t;
     s_s = blockIdx.x - p0;
@@ -1222,7 +1256,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   }
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (n_ids == 0) {
-    if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+    if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
     return false;
   }
   if (m == 0) {
@@ -1232,7 +1266,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
   }
   const int psh = part_shift(n_ids, PD_Y);  // as launch_part_gather with n_rank = n_ids
   if (yhist) (void)hipMemsetAsync(yhist, 0, PD_Y * 4, s);
-  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
   uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   uint64_t cw = (uint64_t)NB * nchunks;
   uint32_t* counts = tmp;
@@ -1290,7 +1324,7 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
   unsigned long long* bcap = bcur + DEGB_NB;
   uint16_t* ep = (uint16_t*)(((uintptr_t)(bcap + DEGB_NB + 1) + 15) & ~(uintptr_t)15);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
-  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
   (void)hipMemsetAsync(scnt, 0, 2 * DEGB_NB * 4, s);
   const int psh = part_shift(n_ids, PD_Y);  // the first partition pass's y digits
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
@@ -1332,6 +1366,8 @@ bool front_fused_ok(uint64_t m, uint32_t n_ids) {
          part_shift(n_ids, PD_Y) == SH && SH <= 16 && NB <= DEGB_NB;
 }
 
+// the histogram's slice length: about 2m / 1024 entries (at least 2^20), 4 slices per CU
+static uint64_t hist16s_ch(uint64_t m) { return std::max<uint64_t>(1ull << 20, (2 * m + 1023) / 1024); }
 bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                         uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                         uint32_t* part_ws, uint64_t* mid, uint64_t mid_slots, uint32_t* stats,
@@ -1348,7 +1384,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   unsigned long long* ys64 = bcap + DEGB_NB + 1;
   uint16_t* ep = (uint16_t*)(((uintptr_t)(ys64 + DEGB_NB + 1) + 15) & ~(uintptr_t)15);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
-  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
   (void)hipMemsetAsync(scnt, 0, 2 * DEGB_NB * 4, s);
   (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
@@ -1372,8 +1408,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   if (mark) mark(mark_arg, "front_fused");
   // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
   if (SH > 15) {
-    // slices of about 2m / 1024 entries (at least 2^20): 4 slices per CU over 256 CUs
-    const uint64_t CH = std::max<uint64_t>(1ull << 20, (2 * m + 1023) / 1024);
+    const uint64_t CH = hist16s_ch(m);
     const unsigned grid = (unsigned)(NB + (2 * m + CH - 1) / CH + 1);
     (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
     hipLaunchKernelGGL(k_degb_hist16s, dim3(grid), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
@@ -1585,7 +1620,7 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
   auto align16 = [](void* p) { return (uint16_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15); };
   uint16_t* epx = align16(bx + NB + 2);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
-  if (stats) (void)hipMemsetAsync(stats, 0, 8, s);
+  if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
   (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
   const int psh = part_shift(n_ids, PD_X);  // as launch_part_second with n_rank = n_ids
   hipLaunchKernelGGL(k_fh_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
@@ -2110,6 +2145,7 @@ void launch_nsd_selfloops(const uint32_t* selfc, uint32_t n_ids, const uint32_t*
 // ---------------------------------------------------------------------------------------
 static constexpr int SQ_DB = 10;
 static constexpr uint32_t SQ_T = 1u << SQ_DB;  // == the block size: one class per thread
+static_assert(SQ_T == SEQ_BIG, "the degree stats count the radix-sorted tail's ids");
 static constexpr int SQ_IT = 16;
 static constexpr uint32_t SQ_CHUNK = 1024u * SQ_IT;
 static constexpr uint32_t SQ_G = 16;  // chunks per group of tm_offsets' column and row passes
