@@ -1153,56 +1153,95 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
   const uint64_t x0 = xs[b], x1 = max(x0, min(xs[b + 1], xf[b]));
   const uint64_t y0 = ys[b], y1 = max(y0, min(ys[b + 1], yf[b]));
   const uint64_t v0 = (uint64_t)sl * CH, v1 = min(v0 + CH, (x1 - x0) + (y1 - y0));
-  uint32_t acc[64];
+  // Rounds of RW = 65528 entries (8191 16-B loads: thread 1023 skips its eighth, so a round
+  // counts at most 65528 < 65536 of one id into a u16 half) from the 8-aligned entry below the
+  // segment's start, in two halves of four loads per thread.  The next round's first half is
+  // loaded right after this round's counting, so that it is in flight during the fold (which
+  // reads and clears each counter word once: ids 2w and 2w + 1 of word w) — the zeroing pass
+  // and one barrier per round are gone too.  RMAT-26 histogram 2.03 -> 1.72 ms, twitter shape
+  // 3.31 -> 2.84 ms (profiles/r05/t_hist_rounds/; 65535-entry segments with a zeroing pass, a
+  // separate fold and the loads issued only inside the count before).
+  constexpr uint64_t RW = 65528;
+  uint32_t lo[32], hi[32];
 #pragma unroll
-  for (int k = 0; k < 64; ++k) acc[k] = 0;
-  constexpr int V = 4;
+  for (int k = 0; k < 32; ++k) { lo[k] = 0; hi[k] = 0; }
+  for (uint32_t i = t; i < 32768; i += DEGB_THREADS) pk[i] = 0;
+  block_sync();
   for (int sg = 0; sg < 2; ++sg) {
-    // this slice's part of segment sg (virtual entries [v0, v1) over x then y)
     const uint64_t off = sg ? (x1 - x0) : 0, len = sg ? (y1 - y0) : (x1 - x0);
     const uint64_t a = min(max(v0, off), off + len) - off, e = min(max(v1, off), off + len) - off;
-    if (a >= e) continue;
+    if (a >= e) continue;  // (uniform)
     const uint16_t* __restrict__ src = sg ? ey : ex;
     const uint64_t s0 = (sg ? y0 : x0) + a, s1 = (sg ? y0 : x0) + e;
-    for (uint64_t g0 = s0; g0 < s1; g0 += 65535) {
-      const uint64_t g1 = min(g0 + 65535, s1);
-      for (uint32_t i = t; i < 32768; i += DEGB_THREADS) pk[i] = 0;
-      block_sync();
-      for (uint64_t i0 = g0 & ~7ull; i0 < g1; i0 += 8 * V * DEGB_THREADS) {
-        uint4 q[V];
+    const uint64_t A = s0 & ~7ull, last = (s1 - 1) & ~7ull;
+    const uint64_t nr = (s1 - A + RW - 1) / RW;
+    uint4 q[4];
+    // (offsets within a round in u32, from the round's uniform base pointer; half h of a
+    // round = loads u = 4h .. 4h + 3)
+    auto load_half = [&](uint64_t r, int h) {  // unpredicated: clamped to the last 8-entry group
+      const uint64_t rb = A + r * RW;
+      const uint16_t* rp = src + rb;
+      const uint32_t lim = (uint32_t)(last - rb);
+      uint32_t tt = t;
+      asm volatile("" : "+v"(tt));
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-          const uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + t);
-          q[u] = i < g1 ? *(const uint4*)(src + i) : make_uint4(0, 0, 0, 0);
-        }
+      for (int u = 0; u < 4; ++u)
+        q[u] = *(const uint4*)(rp + min(8u * ((uint32_t)(4 * h + u) * DEGB_THREADS + tt), lim));
+    };
+    auto count_half = [&](uint32_t r0, uint32_t r1, int h) {
+      uint32_t tt = t;
+      asm volatile("" : "+v"(tt));  // (keeps the 32 positions from being hoisted and spilled)
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-          const uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + t);
-          const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t i = 8u * ((uint32_t)(4 * h + u) * DEGB_THREADS + tt);
+        const bool inr = h == 0 || u < 3 || t < DEGB_THREADS - 1;
+        const uint32_t wv[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint64_t ik = i + k;
-            const uint32_t v = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-            if (ik >= g0 && ik < g1) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
-          }
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t ik = i + k;
+          const uint32_t v = (wv[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+          if (inr && ik >= r0 && ik < r1) atomicAdd(&pk[v >> 1], 1u << (16 * (v & 1)));
         }
       }
+    };
+    load_half(0, 0);
+    for (uint64_t r = 0; r < nr; ++r) {
+      const uint64_t rb = A + r * RW;
+      const uint32_t r0 = (uint32_t)(max(s0, rb) - rb), r1 = (uint32_t)(min(s1, rb + RW) - rb);
+      count_half(r0, r1, 0);
+      if (r1 > 32768) {  // (uniform)
+        load_half(r, 1);
+        count_half(r0, r1, 1);
+      }
+      if (r + 1 < nr) load_half(r + 1, 0);  // in flight during the fold
       block_sync();
 #pragma unroll
-      for (int k = 0; k < 64; ++k) {
-        const uint32_t id = (uint32_t)k * DEGB_THREADS + t;
-        acc[k] += (pk[id >> 1] >> (16 * (id & 1))) & 0xFFFFu;
+      for (int k = 0; k < 32; ++k) {
+        const uint32_t wd = (uint32_t)k * DEGB_THREADS + t;
+        const uint32_t v = pk[wd];
+        pk[wd] = 0;
+        lo[k] += v & 0xFFFFu;
+        hi[k] += v >> 16;
+        // (batches of 8 reads: all 32 in flight beside the prefetched loads would spill)
+        if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
       }
       block_sync();
     }
   }
   const uint64_t base = (uint64_t)b << 16;
 #pragma unroll
-  for (int k = 0; k < 64; ++k) {
-    const uint64_t id = base + (uint64_t)k * DEGB_THREADS + t;
-    if (id < n_ids) {
-      if (nsl == 1) deg[id] = acc[k];
-      else if (acc[k]) atomicAdd(&deg[id], acc[k]);
+  for (int k = 0; k < 32; ++k) {
+    const uint64_t id = base + 2 * ((uint64_t)k * DEGB_THREADS + t);
+    if (id + 1 < n_ids) {
+      if (nsl == 1) {
+        *(uint2*)(deg + id) = make_uint2(lo[k], hi[k]);
+      } else {
+        if (lo[k]) atomicAdd(&deg[id], lo[k]);
+        if (hi[k]) atomicAdd(&deg[id + 1], hi[k]);
+      }
+    } else if (id < n_ids) {
+      if (nsl == 1) deg[id] = lo[k];
+      else if (lo[k]) atomicAdd(&deg[id], lo[k]);
     }
   }
 }
