@@ -889,7 +889,7 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
   }
 }
 
-__global__ void __launch_bounds__(DEGB_THREADS)
+__global__ void __launch_bounds__(DEGB_THREADS, 8)  // (8 waves per SIMD, two blocks per CU: <= 64 VGPRs)
 k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offsets,
             const uint32_t* __restrict__ counts, uint32_t nchunks, uint32_t NB, int SH, uint32_t H,
             uint32_t n_ids, uint32_t* __restrict__ deg, const unsigned long long* __restrict__ bstart,
@@ -898,7 +898,9 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
             const uint64_t* __restrict__ rec0 = nullptr,
             const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */,
             const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */) {
-  __shared__ uint32_t cnt[DEGB_HALF];
+  // span words of dynamic LDS (degb_hist_lds): 16 KB for R-MAT-22's 4096-id buckets, where a
+  // fixed 128 KB array held the CU to one block
+  extern __shared__ uint32_t cnt[];
   const uint32_t b = blockIdx.x / H, h = blockIdx.x % H;
   const uint32_t span = H > 1 ? DEGB_HALF : (1u << SH);
   for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) cnt[i] = 0;
@@ -936,14 +938,24 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
   // 32 entries (four 16-B loads, all issued before use: the loop is latency-bound otherwise)
   // per thread per iteration, from the 8-aligned entry below s0 (ep is padded: the loads may
   // run up to 7 entries past the end)
+  // The next iteration's loads are issued before this one's entries are counted (registers
+  // double-buffered; clamped to the last 8-entry group, used only below s1).
   constexpr int V = 4;
+  const uint64_t ilast = s1 > s0 ? (s1 - 1) & ~7ull : 0;
+  uint4 nq[V];
+  auto load_it = [&](uint64_t i0) {
+    uint32_t tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));  // (not hoisted: registers for two blocks per CU)
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+      nq[u] = *(const uint4*)(ep_s + min(i0 + 8 * ((uint64_t)u * DEGB_THREADS + tt), ilast));
+  };
+  if (s0 < s1) load_it(s0 & ~7ull);
   for (uint64_t i0 = s0 & ~7ull; i0 < s1; i0 += 8 * V * DEGB_THREADS) {
     uint4 q[V];
 #pragma unroll
-    for (int u = 0; u < V; ++u) {
-      uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
-      q[u] = i < s1 ? *(const uint4*)(ep_s + i) : make_uint4(0, 0, 0, 0);
-    }
+    for (int u = 0; u < V; ++u) q[u] = nq[u];
+    if (i0 + 8 * V * DEGB_THREADS < s1) load_it(i0 + 8 * V * DEGB_THREADS);
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       uint64_t i = i0 + 8 * ((uint64_t)u * DEGB_THREADS + threadIdx.x);
@@ -985,6 +997,11 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
       big += d >= SEQ_BIG;
     }
   if (stats) deg_stats_flush(stats, mx, zeros, big);
+}
+
+// Dynamic LDS of k_degb_hist: its counters, one word per id of a bucket (or of a half).
+static size_t degb_hist_lds(int SH, uint32_t H) {
+  return (size_t)(H > 1 ? DEGB_HALF : (1u << SH)) * 4;
 }
 
 // Buckets of 65536 ids (n_ids > 2^25): one workgroup per bucket reads the bucket's run ONCE
@@ -1333,7 +1350,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, n_ids, deg,
                        (const unsigned long long*)bstart, stats, DEGB_PLAIN16);
   else
-    hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB * H), dim3(DEGB_THREADS), degb_hist_lds(SH, H), s, (const uint16_t*)ep,
                        (const uint32_t*)offsets, (const uint32_t*)counts, nchunks, NB, SH, H, n_ids,
                        deg, (const unsigned long long*)bstart, stats, DEGB_PLAIN_SMALL);
   return yhist != nullptr;
@@ -1385,7 +1402,7 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
                        (const unsigned long long*)nullptr, (const uint64_t*)nullptr,
                        (const unsigned long long*)bcur);
   else
-    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), degb_hist_lds(SH, 1), s, (const uint16_t*)ep,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, SH, 1u, n_ids,
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)nullptr, (const unsigned long long*)nullptr,
@@ -1456,7 +1473,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                        (const unsigned long long*)ycur, NB, n_ids, CH, deg);
     if (stats) launch_deg_stats(deg, n_ids, stats, s);
   } else
-    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), degb_hist_lds(SH, 1), s, (const uint16_t*)ep,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, NB, SH, 1u, n_ids,
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)ob, (const unsigned long long*)ys64,
@@ -1677,7 +1694,7 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
                        (const unsigned long long*)by, stats, DEGB_PLAIN16,
                        (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
   else
-    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), 0, s, (const uint16_t*)nullptr,
+    hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), degb_hist_lds(SH, 1), s, (const uint16_t*)nullptr,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr, nchunks, NB, SH, 1u,
                        n_ids, deg, (const unsigned long long*)by, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)epx, (const unsigned long long*)bx, (const uint64_t*)recs);
