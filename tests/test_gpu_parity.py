@@ -260,6 +260,38 @@ def test_graph2tree_dev_fused_64k_buckets(oracle, gpu, options, n, m, mode):
     assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_graph2tree_dev_fused_hub_fills_rounds(oracle, gpu, mode):
+    """The fused pass's histogram counts a bucket in rounds of 65528 entries into u16 halves:
+    a hub that is the ONLY id of its 64K-id bucket (35 % of 2^25 + 12345 records) fills every
+    round of that bucket's endpoint region with itself, 65528 counts a round — one short of
+    wrapping a half. Its degree (~11.7 M) and the tree must match the checker."""
+    import torch
+    from sheep_amd import capi, device
+
+    rng = np.random.default_rng(11 + mode)
+    n = (1 << 26) - 5
+    m = (1 << 25) + 12345
+    uv = rng.integers(0, n, size=(m, 2)).astype(np.uint32)
+    hb = 5  # no other id of bucket 5 occurs
+    for c in (0, 1):
+        inb = (uv[:, c] >> 16) == hb
+        uv[inb, c] += 1 << 16
+    hub = (hb << 16) + 9
+    sel = rng.random(m) < 0.35
+    uv[sel, 0] = hub
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    s_d, p_d, w_d, k = device.graph2tree(uv_d, n, mode)
+    torch.cuda.synchronize()
+    assert "front_fused" in dict(capi.last_timings())
+    seq = oracle.degree_sequence(uv, mode)
+    p, w = oracle.build_tree(uv, seq)
+    assert k == len(seq) and seq[-1] == hub
+    assert np.array_equal(s_d[:k].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:k].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:k].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("n,mode", [(3000017, 0), (40000003, 1)])
 def test_graph2tree_dev_fused_ragged_ids(oracle, gpu, n, mode):
     """The default front half (the fused pass, sampled capacities) on id spaces that are not a
