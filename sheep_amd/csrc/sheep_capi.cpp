@@ -45,6 +45,7 @@ static const KnobDef kKnobs[] = {
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
     {"kb_merge", &Knobs::kb_merge},       {"lab", &Knobs::lab},
+    {"kb_fresh_lo", &Knobs::kb_fresh_lo}, {"kb_fresh_hi", &Knobs::kb_fresh_hi},
 };
 
 static Knobs g_knobs;
@@ -514,8 +515,8 @@ static std::vector<char> birth_window(const std::vector<std::pair<uint32_t, uint
   for (size_t k = 0; k + 1 < nbk; ++k) {
     E += (double)recs(k);
     const double B = (double)bk[k + 1].first, d = B > 0 ? 2.0 * E / B : 0.0;
-    if (d >= 0.5) fresh[k + 1] = 1;
-    if (d >= 1.0) break;
+    if (d >= knobs().kb_fresh_lo / 100.0) fresh[k + 1] = 1;
+    if (d >= knobs().kb_fresh_hi / 100.0) break;
   }
   return fresh;
 }

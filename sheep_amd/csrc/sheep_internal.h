@@ -58,6 +58,8 @@ struct Knobs {
                          //   most kb_merge / 10000 of the records (0: off;
                          //   the lockstep loop: 20 unless off)
   int lab = 0;           // SHEEP_LAB: bit mask of kernel variants under A/B (lab only)
+  int kb_fresh_lo = 50;  // SHEEP_KB_FRESH_LO / _HI: the kb loop's birth window, in hundredths of
+  int kb_fresh_hi = 100; //   the mean degree 2E/B below a bucket's end (tree_from_sorted)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
