@@ -282,7 +282,9 @@ def main():
             "data": data,
             "config": dict(wl, records=m, n_ids=n_ids, n_seq=n_seq,
                            parallelism=("edge-shard x%d (%s)" % (world, args.dist)
-                                        if world > 1 else "single")),
+                                        if world > 1 else
+                                        "lockstep driver, one-rank RCCL group" if args.lockstep_1
+                                        else "single")),
             "path_roofline": {"bytes": path_bytes,
                               "frac": path_bytes / (elapsed / args.steps) / (world * HBM_PEAK),
                               "bytes_nseq": 16 * m + 24 * n_seq},
