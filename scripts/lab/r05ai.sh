@@ -1,0 +1,8 @@
+# Check at the dense-cuts default: the GPU suite, smoke(), and the four bench lines.
+export TMPDIR=/tmp
+O=gpurun_out/r05ai; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+OUT=$O TESTS=0 bash scripts/gpu_round.sh || exit 1

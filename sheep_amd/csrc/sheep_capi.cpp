@@ -457,10 +457,20 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 // Edge-quantile cuts: 2/5 as many (at least 8): with the rank cuts at 40 and the device-picked
 // anchor, K_e = 8/12/16/24/32/40 -> RMAT-26 tree 19.2/19.0/18.9/19.1/19.4/19.7 ms, twitter shape
 // (12/16/24/40) 28.4/28.3/29.1/29.4 ms, RMAT-25 (16/40) 11.6/12.5 ms (lab_kcuts.jsonl).
-static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 40) {
+static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 40,
+                      uint32_t n_seq = 0) {
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
   *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : std::max<uint32_t>(8, K_auto * 2 / 5);
   *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
+  // Dense graphs (mean degree >= 40) of 2^26 .. 2^27 records: 12 rank cuts instead of 8.
+  // Step ms, default -> 12 (profiles/r05/ah_dense_cuts/): R-MAT-22 seeds 22 / 1 / 2 / 5 / 9
+  // 4.10 / 4.15 / 4.43 / 4.18 / 4.10 -> 3.93 / 3.98 / 4.07 / 4.03 / 3.89 (its percolation
+  // bucket's zipper: 10.3 M -> 1.0 M steps).  Outside that size class the same cuts are mixed
+  // (R-MAT-21 +0.09, R-MAT-23 seeds 23 / 7 -0.45 / -0.05, R-MAT-24 seeds 24 / 3 -0.59 / +1.16
+  // ms), and the LJ shape (mean degree 28) loses 2.5 ms at any other count.
+  if (n_seq && m >= (1ull << 26) && m < (1ull << 27) && 2 * m >= 40ull * n_seq &&
+      knobs().kb_rankb <= 0 && knobs().kb_buckets <= 0)
+    *K_r = 12;
 }
 
 // Directly binned records (launch_edge_bin): the buckets' .second are bin indices, bucket k's
@@ -528,7 +538,7 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
                              const uint32_t* bins = nullptr, uint32_t nb = 0,
                              const SegPlan* seg = nullptr) {
   uint32_t K_e, K_r;
-  kb_counts(m, &K_e, &K_r);
+  kb_counts(m, &K_e, &K_r, 40, n_seq);
   uint32_t K = K_e + K_r;
   // parent and hint interleaved (pj[2v], pj[2v + 1]): a zipper step loads one line; the parents
   // go to d_parent after the loop
@@ -784,7 +794,7 @@ static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
   if (merge < 0) merge = knobs().kb_merge;
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
-  kb_counts(m, &K_e, &K_r, kmax);
+  kb_counts(m, &K_e, &K_r, kmax, n_seq);
   std::vector<uint32_t> cuts;
   for (uint32_t k = 1; k < K_e; ++k) {
     const uint64_t target = m_valid * k / K_e;
