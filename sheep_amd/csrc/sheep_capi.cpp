@@ -462,13 +462,13 @@ static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
   *K_e = knobs().kb_buckets > 0 ? (uint32_t)knobs().kb_buckets : std::max<uint32_t>(8, K_auto * 2 / 5);
   *K_r = knobs().kb_rankb > 0 ? (uint32_t)knobs().kb_rankb : K_auto;
-  // Dense graphs (mean degree >= 40) of 2^26 .. 2^27 records: 12 rank cuts instead of 8.
-  // Step ms, default -> 12 (profiles/r05/ah_dense_cuts/): R-MAT-22 seeds 22 / 1 / 2 / 5 / 9
-  // 4.10 / 4.15 / 4.43 / 4.18 / 4.10 -> 3.93 / 3.98 / 4.07 / 4.03 / 3.89 (its percolation
-  // bucket's zipper: 10.3 M -> 1.0 M steps).  Outside that size class the same cuts are mixed
-  // (R-MAT-21 +0.09, R-MAT-23 seeds 23 / 7 -0.45 / -0.05, R-MAT-24 seeds 24 / 3 -0.59 / +1.16
-  // ms), and the LJ shape (mean degree 28) loses 2.5 ms at any other count.
-  if (n_seq && m >= (1ull << 26) && m < (1ull << 27) && 2 * m >= 40ull * n_seq &&
+  // Dense graphs (mean degree >= 40) of 1.5 x 2^25 .. 1.5 x 2^27 records: 12 rank cuts
+  // (instead of 8 .. 23).  Step ms, default -> 12 (profiles/r05/ah_dense_cuts/): R-MAT-22 seeds
+  // 22 / 1 / 2 / 5 / 9 4.10 / 4.15 / 4.43 / 4.18 / 4.10 -> 3.93 / 3.98 / 4.07 / 4.03 / 3.89 (its
+  // percolation bucket's zipper: 10.3 M -> 1.0 M steps), R-MAT-23 seeds 23 / 7 6.77 / 6.65 ->
+  // 6.32 / 6.60.  Either side the same cuts are mixed (R-MAT-21 +0.09 ms; R-MAT-24 seeds 24 / 3
+  // -0.59 / +1.16 ms), and the LJ shape (mean degree 28) loses 0.2-2.5 ms at any other count.
+  if (n_seq && m >= (3ull << 24) && m < (3ull << 26) && 2 * m >= 40ull * n_seq &&
       knobs().kb_rankb <= 0 && knobs().kb_buckets <= 0)
     *K_r = 12;
 }
