@@ -1,6 +1,6 @@
 # Round-5 final check at HEAD: the GPU suite, smoke(), the default bench line.
 export TMPDIR=/tmp
-O=gpurun_out/final5; mkdir -p $O
+O=gpurun_out/${FINAL_DIR:-final5}; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
