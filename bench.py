@@ -105,7 +105,7 @@ def cpu_baseline_ir(scale, edgefactor, seed, threads):
                                                            sort_s, map_s, red_s, cpu_model())}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -132,13 +132,67 @@ def main():
     # N = 1 through the N > 1 code: the C++ multi-rank driver over a one-rank RCCL group, to
     # measure its host overhead and collective launches on one GPU (not the default N = 1 path)
     ap.add_argument("--lockstep-1", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+# The rank setup below is shared by main() and tests/test_bench_ranks.py, which runs it over
+# gloo process groups of 2 / 4 / 8 CPU ranks with the GPU calls stubbed (no 8-GPU node here).
+def rank_env(gpus):
+    """(world, rank, local) from the launcher's environment (torch.distributed.run)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if world != gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (gpus, world))
+    return world, rank, local
+
+
+def load_shard(args, rank, world, dev):
+    """This rank's contiguous record range [lo, hi) of the workload (graph2tree -l rank+1/world),
+    generated in HBM by `dev` (sheep_amd.device): (uv, m, n_ids, lo, hi, workload, data)."""
+    from sheep_amd.dist import shard_bounds
+
+    scale, ef, seed = args.scale, args.edgefactor, args.seed
+    if args.workload == "rmat":
+        m = ef << scale
+        n_ids = 1 << scale
+        lo, hi = shard_bounds(m, rank, world)
+        uv = dev.rmat(scale, ef, seed, lo, hi)  # this rank's records, resident in HBM
+        wl = {"workload": "rmat%d_ef%d" % (scale, ef), "scale": scale, "edgefactor": ef,
+              "seed": seed}
+        data = "synthetic R-MAT (Graph500 A/B/C/D .57/.19/.19/.05), generated in HBM"
+    else:
+        n_ids, m, gamma, i0, seed = dev.POWERLAW[args.workload]
+        lo, hi = shard_bounds(m, rank, world)
+        uv = dev.powerlaw(n_ids, m, gamma, i0, seed, lo, hi)
+        wl = {"workload": "%s_shape_powerlaw" % args.workload, "gamma": gamma, "i0": i0,
+              "seed": seed}
+        data = ("synthetic power-law (Chung-Lu, P(i) ~ (i+%g)^-1/(%g-1)), %s-shape n and m, "
+                "generated in HBM" % (i0, gamma, args.workload))
+    return uv, m, n_ids, lo, hi, wl, data
+
+
+def native_driver(args, world):
+    """Whether the step is the C++ multi-rank driver over its own RCCL communicator (the
+    default for N > 1); the Python orchestration rehearses it where RCCL cannot run (gloo ranks
+    sharing one device)."""
+    return (world > 1 and args.dist == "lockstep" and args.backend == "nccl"
+            and not args.same_device) or args.lockstep_1
+
+
+def join_comm(rank, world, dev):
+    """Rank 0 makes the RCCL id, the torch process group carries it to every rank, and each rank
+    joins the library's communicator as (id, world, rank).  Returns the id."""
+    uid = [dev.comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    dev.comm_init(uid[0], world, rank)
+    return uid[0]
+
+
+def main():
+    args = parse_args()
+    world, rank, local = rank_env(args.gpus)
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)
@@ -153,40 +207,18 @@ def main():
             dist.init_process_group("gloo")
 
     from sheep_amd import capi, device
-    from sheep_amd.dist import DeviceOps, build_tree_lockstep, build_tree_sharded, shard_bounds
+    from sheep_amd.dist import DeviceOps, build_tree_lockstep, build_tree_sharded
 
     device.init(local)
     scale, ef, seed = args.scale, args.edgefactor, args.seed
-    if args.workload == "rmat":
-        m = ef << scale
-        n_ids = 1 << scale
-        lo, hi = shard_bounds(m, rank, world)
-        uv = device.rmat(scale, ef, seed, lo, hi)  # this rank's records, resident in HBM
-        wl = {"workload": "rmat%d_ef%d" % (scale, ef), "scale": scale, "edgefactor": ef,
-              "seed": seed}
-        data = "synthetic R-MAT (Graph500 A/B/C/D .57/.19/.19/.05), generated in HBM"
-    else:
-        n_ids, m, gamma, i0, seed = device.POWERLAW[args.workload]
-        lo, hi = shard_bounds(m, rank, world)
-        uv = device.powerlaw(n_ids, m, gamma, i0, seed, lo, hi)
-        wl = {"workload": "%s_shape_powerlaw" % args.workload, "gamma": gamma, "i0": i0,
-              "seed": seed}
-        data = ("synthetic power-law (Chung-Lu, P(i) ~ (i+%g)^-1/(%g-1)), %s-shape n and m, "
-                "generated in HBM" % (i0, gamma, args.workload))
+    uv, m, n_ids, lo, hi, wl, data = load_shard(args, rank, world, device)
     torch.cuda.synchronize()
     ops = DeviceOps()
-    # the C++ multi-rank driver joins its own RCCL communicator (the id travels over the torch
-    # process group); the Python orchestration rehearses it where RCCL cannot run (gloo ranks
-    # sharing one device)
-    native = (world > 1 and args.dist == "lockstep" and args.backend == "nccl"
-              and not args.same_device) or args.lockstep_1
+    native = native_driver(args, world)
     if world > 1 and args.dist == "lockstep" and not native:
         args.dist = "lockstep-py"
     if native:
-        uid = [device.comm_unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        device.comm_init(uid[0], world, rank)
+        join_comm(rank, world, device)
 
     def barrier():
         if world > 1:

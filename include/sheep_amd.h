@@ -13,7 +13,10 @@
  *   - host-pointer calls are synchronous; *_dev calls take device pointers and a HIP stream
  *     (hipStream_t passed as void*; NULL = HIP's default stream, as everywhere in HIP) and
  *     return when the work is ENQUEUED, except where documented as synchronising;
- *   - calls are not re-entrant per device.
+ *   - calls are not re-entrant per device.  Threads: a device's context (its scratch, streams
+ *     and pinned words) serves one caller at a time — two host threads driving the same device
+ *     at once must serialise their calls themselves (the timing-event pool alone is locked);
+ *     the n_ranks rehearsal entry points below give each rank thread a context of its own.
  *
  * Types follow lib/defs.h:76-82: ids, jnids and weights are uint32, INVALID = 0xFFFFFFFF.
  * An edge stream is m records of (tail, head) as 2*m uint32 (the XS1 weight is dropped).

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 288eb22: SHEEP_LAB 128 / 256 (birth-window weights) were built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: the birth window (fresh anchors) and the sweep plan weigh a directly binned bucket by
 # SHEEP_LAB=128 its estimated records, SHEEP_LAB=256 its exact records (the bins' fill, read
 # back with the overflow words) instead of its capacity (which adds 5 % + 8192 slots per bin).

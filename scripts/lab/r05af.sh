@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 7217ac4: SHEEP_LAB 512 (tile-relative write-out bases) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: SHEEP_LAB=512 = tile-relative write-out bases in the fused pass (y: base + slot while the
 # slot is below the run's end; x: base + slot) and the edge pass (base + slot): one LDS table
 # read fewer per written record.

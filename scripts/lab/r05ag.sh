@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit e825ef2: SHEEP_LAB 1024 (deferred kept-pair writes in k_kb_map) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: SHEEP_LAB=1024 = k_kb_map writes chunk j's kept pairs during chunk j + 1 (no wave waits
 # for the chunk's reservation, a returning atomic on one counter shared by every block).
 # Hypothesis: the reservation's round trip is exposed once per chunk (all waves wait at the

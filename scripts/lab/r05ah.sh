@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 731ab19: SHEEP_LAB 2048 (12 rank cuts for dense graphs) was built in the gitignored csrc_lab copy; adopted as kb_counts' dense rule (sheep_capi.cpp). The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: SHEEP_LAB=2048 = 12 rank cuts + 8 edge cuts for dense graphs (mean degree >= 40) below
 # 2^29 records (R-MAT 21-24; LJ's mean degree 28 keeps the default).  Across seeds and scales.
 export TMPDIR=/tmp

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 0bc0256: SHEEP_LAB 128 (estimate-weighted birth window) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B on top of the dense rank cuts: SHEEP_LAB=128 = the birth window and sweeps weigh a binned
 # bucket by its estimated records (no capacity slack).
 export TMPDIR=/tmp

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 173f10d: the giant-sweep schedules (SHEEP_LAB_SWEEP*) were built in the gitignored csrc_lab copy; adopted as the sweeps on the applies' stream (sweep_plan). The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 export TMPDIR=/tmp
 O=gpurun_out/r05f; mkdir -p $O
 OUT=$O bash scripts/ab_env.sh "--steps 8 --warmup 2 --no-cpu-baseline" - SHEEP_LAB_SWEEP=1 SHEEP_LAB_SWEEP=2 SHEEP_LAB_SWEEP=3 SHEEP_LAB_SWEEP=4 || exit 1

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit df0b782: the birth-window split (SHEEP_LAB_BIRTH_SPLIT) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 export TMPDIR=/tmp
 O=gpurun_out/r05l; mkdir -p $O
 OUT=$O bash scripts/ab_env.sh "--scale 22 --seed 22 --check --steps 20 --warmup 3 --no-cpu-baseline" - SHEEP_LAB_BIRTH_SPLIT=2 SHEEP_LAB_BIRTH_SPLIT=4 || exit 1

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 67647ab: the sparse-word sweep skip (SHEEP_LAB_SWEEP_MINPOP) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 export TMPDIR=/tmp
 O=gpurun_out/r05m; mkdir -p $O
 OUT=$O bash scripts/ab_env.sh "--steps 8 --warmup 2 --no-cpu-baseline" - SHEEP_LAB_SWEEP_MINPOP=1 SHEEP_LAB_SWEEP_MINPOP=8 SHEEP_LAB_SWEEP_MINPOP=24 - || exit 1

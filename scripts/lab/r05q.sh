@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 5b56007: SHEEP_LAB bits 1 / 2 (persistent fused pass, Eytzinger bin search) were built in the gitignored csrc_lab copy; both adopted. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # Lab A/B: SHEEP_LAB bit 1 = persistent fused front pass with the next tile's records loaded
 # under the y write-out; bit 2 = k_edge_bin's bin search over an Eytzinger-ordered table.
 # The GPU suite runs once with both on, then bench lines alternate the settings.

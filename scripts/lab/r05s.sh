@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit e40dfd7: SHEEP_LAB 4 (split histogram buckets through partial counts) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # GPU suite on the readback merge (fused pass: error / overflow words with the degree stats;
 # the sequence's radix tail sized from the stats); the suite again with SHEEP_LAB=4 (split
 # histogram buckets through partial counts + k_degb_combine instead of global atomics); then

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit 99fef59: SHEEP_LAB 8 (histogram rounds with the next loads in flight) was built in the gitignored csrc_lab copy; adopted. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: SHEEP_LAB=8 = k_degb_hist16s in rounds of 65528 entries with the next round's first
 # half loaded during the fold, the fold clearing the counters (no zeroing pass).
 export TMPDIR=/tmp

@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit cb15880: SHEEP_LAB 16 / 32 (fused-pass grid and write order) were built in the gitignored csrc_lab copy; measurement only, neither adopted. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # Fused pass: WRITE_SIZE and time with the persistent grid (default) and one block per tile
 # (SHEEP_LAB=16) and y runs written before x runs (SHEEP_LAB=32)
 export TMPDIR=/tmp

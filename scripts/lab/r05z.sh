@@ -1,3 +1,5 @@
+# (round 6) Added with its results in commit b73dd66: SHEEP_LAB 64 (second partition pass as 1024 x 8) was built in the gitignored csrc_lab copy; dropped. The SHEEP_LAB knob is gone, so
+# re-running this script now compares identical code.
 # A/B: SHEEP_LAB=64 = the second partition pass as 1024 threads x 8 records (32 waves per CU,
 # 60 VGPRs) instead of 512 x 16 (16 waves, 104 VGPRs); same 8192-record tiles and LDS.
 export TMPDIR=/tmp

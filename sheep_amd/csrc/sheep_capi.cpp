@@ -44,7 +44,7 @@ static const KnobDef kKnobs[] = {
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
-    {"kb_merge", &Knobs::kb_merge},       {"lab", &Knobs::lab},
+    {"kb_merge", &Knobs::kb_merge},
     {"kb_fresh_lo", &Knobs::kb_fresh_lo}, {"kb_fresh_hi", &Knobs::kb_fresh_hi},
 };
 
@@ -196,8 +196,10 @@ struct Timer {
   hipStream_t s;
   std::vector<hipEvent_t>* pool;
   std::vector<std::pair<const char*, hipEvent_t>> ev;
-  explicit Timer(hipStream_t st) : s(st), pool(&ctx().ev_pool) { mark("start"); }
+  std::mutex* mu;
+  explicit Timer(hipStream_t st) : s(st), pool(&ctx().ev_pool), mu(&ctx().ev_mu) { mark("start"); }
   hipEvent_t take() {
+    std::lock_guard<std::mutex> lk(*mu);
     if (pool->empty()) {
       hipEvent_t e;
       HIP_CHECK(hipEventCreate(&e));
@@ -251,6 +253,7 @@ struct Timer {
     for (auto& x : host) c.timings.push_back(x);
   }
   ~Timer() {  // (a recorded event may be re-recorded: the pool holds them for the next call)
+    std::lock_guard<std::mutex> lk(*mu);
     for (auto& e : ev) pool->push_back(e.second);
     for (auto& sp : spans) {
       pool->push_back(std::get<1>(sp));
@@ -457,6 +460,8 @@ using Buckets = std::vector<std::pair<uint32_t, uint64_t>>;
 // Edge-quantile cuts: 2/5 as many (at least 8): with the rank cuts at 40 and the device-picked
 // anchor, K_e = 8/12/16/24/32/40 -> RMAT-26 tree 19.2/19.0/18.9/19.1/19.4/19.7 ms, twitter shape
 // (12/16/24/40) 28.4/28.3/29.1/29.4 ms, RMAT-25 (16/40) 11.6/12.5 ms (lab_kcuts.jsonl).
+// n_seq = 0 leaves out the dense-graph rule below: it was tuned on the one-GPU loop only, and
+// the lockstep loop's bucket placement has its own measurements (ls_plan).
 static void kb_counts(uint64_t m, uint32_t* K_e, uint32_t* K_r, uint32_t kmax = 40,
                       uint32_t n_seq = 0) {
   const uint32_t K_auto = (uint32_t)std::min<uint64_t>(kmax, std::max<uint64_t>(8, m >> 23));
@@ -789,12 +794,13 @@ static std::vector<uint32_t> make_bins(const std::vector<uint64_t>& dsum, uint32
 static std::vector<uint32_t> bucket_cuts(const std::vector<uint32_t>& bounds,
                                          const std::vector<unsigned long long>& bin_start,
                                          uint64_t m, uint32_t n_seq, uint32_t kmax = 40,
-                                         int merge = -1 /* kb_merge; -1: the option */) {
+                                         int merge = -1 /* kb_merge; -1: the option */,
+                                         bool one_gpu = true /* kb_counts' dense-graph rule */) {
   const uint32_t nb = (uint32_t)bounds.size();
   if (merge < 0) merge = knobs().kb_merge;
   const uint64_t m_valid = bin_start[nb - 1];
   uint32_t K_e, K_r;
-  kb_counts(m, &K_e, &K_r, kmax, n_seq);
+  kb_counts(m, &K_e, &K_r, kmax, one_gpu ? n_seq : 0);
   std::vector<uint32_t> cuts;
   for (uint32_t k = 1; k < K_e; ++k) {
     const uint64_t target = m_valid * k / K_e;
@@ -1383,7 +1389,7 @@ static void ls_plan(Lockstep& L, const uint64_t* global_counts, uint32_t* nbk_ou
   // the lockstep loop merges at 0.2 %: at the one-GPU loop's 0.35 % the giant of RMAT-26 forms
   // where the P = 8 simulation's tree critical path goes 6.7 -> 16.4 ms
   std::vector<uint32_t> cuts = bucket_cuts(L.bounds, gstart, gstart[nb], L.n_seq, 40,
-                                           knobs().kb_merge > 0 ? 20 : 0);
+                                           knobs().kb_merge > 0 ? 20 : 0, /*one_gpu=*/false);
   std::vector<uint32_t> bi;  // bin index at each bucket start, then nb - 1 (the INVALID bin)
   bi.push_back(0);
   for (uint32_t i : cuts) bi.push_back(i);
@@ -1415,11 +1421,17 @@ static void ls_map(Lockstep& L, uint32_t k, uint64_t* d_send, long long* d_count
   if (L.direct)
     sg = {L.dseg, L.dseg + 512, L.dseg + 1024, (uint32_t)L.bk[k].second,
           (uint32_t)L.bk[k + 1].second};
-  // (d_send holds ms mark words + one pair per record of the bucket: the caller's contract)
+  // d_send holds ms mark words, then at least min(span, m) pair slots — the caller's contract:
+  // multi_tree sizes it by the largest bucket span over the ranks, the Python mirror
+  // (sheep_amd/dist.py) by this shard's records.  The map keeps at most one pair per record
+  // of the bucket, which is at most both, so kept_cap (the kept-pair guard, FAULT bit 4)
+  // bounds the writes by the buffer in either case (the span alone can exceed the
+  // Python buffer, since directly binned spans include the bins' slack).
   const uint64_t e0 = L.direct ? L.cstart[L.bk[k].second] : L.bk[k].second;
   const uint64_t e1 = L.direct ? L.cstart[L.bk[k + 1].second] : L.bk[k + 1].second;
+  const uint64_t kcap = std::min<uint64_t>(e1 - e0, std::max<uint64_t>(L.m, 1));
   launch_kb_map(L.sorted, e0, e1, B0, L.anchor(k),
-                L.uf, L.label, d_send + L.ms, e1 - e0, L.bm_of(k), L.cnt_of(k), 0, L.hcnt,
+                L.uf, L.label, d_send + L.ms, kcap, L.bm_of(k), L.cnt_of(k), 0, L.hcnt,
                 false, L.ws,
                 L.bins, (uint32_t)L.bounds.size(), L.gbits, L.gbits ? L.gx + (k & 1) : nullptr,
                 L.split ? 2 : (int)L.defer, s, L.direct ? &sg : nullptr,

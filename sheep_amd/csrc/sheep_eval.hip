@@ -12,6 +12,11 @@
 //   Vcom_vol = sum_X (|{part X} ∪ nbr parts| - 1) = distinct keys with part != part(X)
 // Balances and edges cut are per-record histograms over the k parts (LDS-privatised).
 // All arithmetic is integer; results are bit-exact with the reference's.
+// The s_waitcnt immediates below are gfx9 encodings (vmcnt bits [3:0] and [15:14], lgkmcnt
+// [11:8]); on another target they would silently mean a different wait.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "sheep_amd kernels are written for gfx950 only"
+#endif
 #include <hip/hip_runtime.h>
 
 #include "sheep_internal.h"

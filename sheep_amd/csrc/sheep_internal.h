@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,7 +58,6 @@ struct Knobs {
   int kb_merge = 35;     // SHEEP_KB_MERGE: merge adjacent kb buckets while together they hold at
                          //   most kb_merge / 10000 of the records (0: off;
                          //   the lockstep loop: 20 unless off)
-  int lab = 0;           // SHEEP_LAB: bit mask of kernel variants under A/B (lab only)
   int kb_fresh_lo = 50;  // SHEEP_KB_FRESH_LO / _HI: the kb loop's birth window, in hundredths of
   int kb_fresh_hi = 100; //   the mean degree 2E/B below a bucket's end (tree_from_sorted)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
@@ -81,6 +81,8 @@ struct Ctx {
   std::vector<std::pair<const char*, double>> timings;
   std::deque<std::string> span_names;  // storage for the "<name>#" timing labels
   std::vector<hipEvent_t> ev_pool;     // timing events of finished calls (Timer), reused
+  std::mutex ev_mu;                    // guards ev_pool (the rest of a context is one caller's at
+                                       // a time: include/sheep_amd.h "Threads")
   int ls_live = 0;                     // live lockstep sessions (sheep_ls_*) on this device
   struct Comm* comm = nullptr;         // this rank's communicator (sheep_comm_init), if any
   // host record ranges declared immutable (sheep_records_register / sheep_records_load_dat)

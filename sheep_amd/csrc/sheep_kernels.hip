@@ -13,6 +13,11 @@
 //                   union-find loop jtree.cpp:73-83 + unionfind.h:46-102
 //   k_merge         associative tree union (jnode.cpp:174-201) with the same insertion
 //   k_rmat          synthetic input generator (rmat.h)
+// The s_waitcnt immediates below are gfx9 encodings (vmcnt bits [3:0] and [15:14], lgkmcnt
+// [11:8]); on another target they would silently mean a different wait.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "sheep_amd kernels are written for gfx950 only"
+#endif
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 

@@ -71,10 +71,10 @@ def test_options_read_once_and_settable_without_gpu():
     for name in ("ls_split", "ls_seq"):  # options added in round 3
         v = capi.set_option(name, 0)
         assert capi.set_option(name, v) == 0
-    # removed in round 3, then in round 4 the A/B-only ones (always on now)
+    # removed in round 3, then in round 4 the A/B-only ones (always on now); round 6 the lab mask
     for gone in ("sort", "bin_tm", "bin_scatter", "ep_plain", "seq_compact", "seq_sort",
                  "part_ysort", "kb_refresh", "kb_gbits", "kb_defer", "degb_plain", "degb_hist",
-                 "kb_pick", "kb_drop"):
+                 "kb_pick", "kb_drop", "lab"):
         with pytest.raises(capi.SheepError):
             capi.set_option(gone, 0)
     with pytest.raises(capi.SheepError):
