@@ -44,11 +44,13 @@ static const KnobDef kKnobs[] = {
     {"bin_direct", &Knobs::bin_direct},   {"bin_slack", &Knobs::bin_slack},
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
-    {"kb_merge", &Knobs::kb_merge},
+    {"kb_merge", &Knobs::kb_merge},       {"ff_groups", &Knobs::ff_groups},
     {"kb_fresh_lo", &Knobs::kb_fresh_lo}, {"kb_fresh_hi", &Knobs::kb_fresh_hi},
 };
 
 static Knobs g_knobs;
+// the fused front pass's tile groups (Knobs::ff_groups), clamped to 1..8
+static uint32_t ff_groups();
 static std::once_flag g_knobs_once;
 
 static void load_knobs_from_env() {
@@ -68,6 +70,8 @@ Knobs& knobs() {
   std::call_once(g_knobs_once, load_knobs_from_env);
   return g_knobs;
 }
+
+static uint32_t ff_groups() { return (uint32_t)std::max(1, std::min(8, knobs().ff_groups)); }
 
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
@@ -899,7 +903,7 @@ static void build_tree_dev(Ctx& c, const uint32_t* d_uv, uint64_t m, const uint3
     if (di && di->part_first_done) {  // pass 1 ran on c.side, beside the sequence sort
       HIP_CHECK(hipStreamWaitEvent(s, c.part_ev[1], 0));
       launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6, di->mid_slots,
-                         di->mid_caps, di->mid_p6);
+                         di->mid_caps, di->mid_p6, ff_groups());
     } else {
       launch_part_gather(d_uv, m, d_rank, n_rank, items, items_b, pws, s, di && di->yhist_ready,
                          pre6);
@@ -1254,7 +1258,7 @@ static void ls_begin(Lockstep& L, const uint32_t* d_uv, uint64_t m, const uint32
       pws = (uint32_t*)sc.get("part_ws", PART_WS_WORDS * 4);
       HIP_CHECK(hipStreamWaitEvent(s, part_done, 0));
       launch_part_second(items, m, d_rank, n_rank, items_b, pws, s, pre6, mid_slots, mid_caps,
-                         mid_p6);
+                         mid_p6, ff_groups());
     } else {
       mid_caps = false;
       pws = (uint32_t*)sc.get("ls_part_ws", PART_WS_WORDS * 4);
@@ -1707,7 +1711,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
   const bool ffused = ov == 4 && m >= (1ull << 25) && use_part(m) && knobs().bin_direct &&
                       knobs().degree != 1 && part_p6_ok(n_ids) && front_fused_ok(m, n_ids) &&
                       degs_tmp_words(m, n_ids) > 1;
-  const uint64_t mid_slots = ffused ? (fs_room(m, 1024) + 7) & ~7ull : m;
+  const uint64_t mid_slots = ffused ? front_fused_slots(m, n_ids, ff_groups()) : m;
   const bool overlap = !ffused && ov != 0 && m > 0 && use_part(m);
   hipEvent_t part_done = nullptr;
   if (ffused) {
@@ -1719,7 +1723,7 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
     uint64_t* mid = (uint64_t*)c.scratch.get("ls_items", std::max<uint64_t>(m, mid_slots) * 8);
     uint32_t* stats = (uint32_t*)c.scratch.get("stats", 16);
     launch_front_fused(d_uv, m, n_ids, mode, deg_local, selfc, c.d_err, tmp, pws, mid, mid_slots,
-                       stats, ovf_deg, c.d_err + 3, s);
+                       stats, ovf_deg, c.d_err + 3, s, nullptr, nullptr, ff_groups());
     HIP_CHECK(hipEventRecord(c.part_ev[1], s));
     part_done = c.part_ev[1];
     // this shard's degrees are complete unless an x bucket outgrew its region (a local
@@ -2103,7 +2107,9 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
                        m >= (1ull << 25) && 2 * m < (1ull << 32) && knobs().degree != 1 &&
                        degs_tmp_words(m, n_ids) > 1;
   // records the mid buffer holds (capacity regions: their largest possible sum)
-  const uint64_t mid_slots = (sampled || ffused) ? (fs_room(m, 1024) + 7) & ~7ull : m;
+  const uint64_t mid_slots = ffused    ? front_fused_slots(m, n_ids, ff_groups())
+                             : sampled ? (fs_room(m, 1024) + 7) & ~7ull
+                                       : m;
   uint32_t* ovf_deg = c.d_err + 2;
   uint32_t* ovf_part = c.d_err + 3;
   if (overlap) HIP_CHECK(hipEventRecord(c.part_ev[0], s));  // in case degree_dev records none
@@ -2116,7 +2122,7 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     uint64_t* mid = (uint64_t*)c.scratch.get("e_items", std::max<uint64_t>(m, mid_slots) * 8);
     launch_front_fused(d_uv, m, n_ids, degree_mode, deg, selfc, c.d_err, tmp, pws, mid, mid_slots,
                        stats, ovf_deg, ovf_part, s,
-                       [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm);
+                       [](void* t, const char* n) { ((Timer*)t)->mark(n); }, &tm, ff_groups());
     tm.mark("degree_hist");
     HIP_CHECK(hipEventRecord(c.part_ev[1], s));
     // One readback: the error word and both overflow words (d_err[0..3]) with the degree stats.

@@ -60,6 +60,9 @@ struct Knobs {
                          //   the lockstep loop: 20 unless off)
   int kb_fresh_lo = 50;  // SHEEP_KB_FRESH_LO / _HI: the kb loop's birth window, in hundredths of
   int kb_fresh_hi = 100; //   the mean degree 2E/B below a bucket's end (tree_from_sorted)
+  int ff_groups = 8;     // SHEEP_FF_GROUPS: tile groups of the fused front pass (1..8): group g's
+                         //   tiles write their own subregion of every region, so a subregion's
+                         //   runs come from one XCD's blocks and merge in its L2 (round 6)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
@@ -187,7 +190,9 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // m u64 scratch, ws: PART_WS_WORDS u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 // ws: y / x digit counts, the first pass's u64 cursors, the u32 region starts of both passes'
 // outputs, the second pass's cursors, the first pass's capacity region ends (sheep_kernels.hip).
-constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024;
+// (+ the fused front pass's subregion tables: 8192 u64 starts + 2, cursors, ends, u32 tile map)
+constexpr size_t PART_WS_WORDS =
+    1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024 + 2 * (8192 + 2) + 4 * 8192 + 8192 + 1;
 // p6: the second pass's records are packed to 6 bytes (sheep_kernels.hip "packed 6-byte
 // records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
 bool part_p6_ok(uint32_t n_rank);
@@ -200,9 +205,11 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
                        uint32_t* ws, hipStream_t s, bool yhist_ready);
 // out6: pre is written packed; caps: mid holds launch_part_first_caps's regions (mid_slots);
 // in6 (with caps): ... launch_front_fused's packed ones.
+// (in6: the tiles follow the fused pass's subregions, G per y digit: launch_front_fused's G.)
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6 = false,
-                        uint64_t mid_slots = 0, bool caps = false, bool in6 = false);
+                        uint64_t mid_slots = 0, bool caps = false, bool in6 = false,
+                        uint32_t G = 1);
 // Sampled capacities (sheep_kernels.hip, "sampled capacities"): the degree pass without a
 // counting read — a 1/256 sample sizes each bucket's and each y digit's capacity region; the
 // y regions go to part_ws for launch_part_first_caps (mid_slots records; the event caps_done
@@ -220,12 +227,16 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
 // ONE read of the records, into sampled capacity regions (mid_slots, a multiple of 8, packed
 // records in mid).  *ovf_x: the degrees need the exact pass; *ovf_y: the partition must be
 // redone from uv.  False when not applicable (front_fused_ok).
+// G (option ff_groups, 1..8): tile groups, each writing its own subregion of every region
+// (sheep_kernels.hip k_front_fused); front_fused_slots: the mid_slots these regions need.
 bool front_fused_ok(uint64_t m, uint32_t n_ids);
+uint64_t front_fused_slots(uint64_t m, uint32_t n_ids, uint32_t G);
 bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                         uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                         uint32_t* part_ws, uint64_t* mid, uint64_t mid_slots, uint32_t* stats,
                         uint32_t* ovf_x, uint32_t* ovf_y, hipStream_t s,
-                        void (*mark)(void*, const char*) = nullptr, void* mark_arg = nullptr);
+                        void (*mark)(void*, const char*) = nullptr, void* mark_arg = nullptr,
+                        uint32_t G = 1);
 void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t* mid,
                             uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s);
 void launch_pst_from_count(const uint32_t* seq, uint32_t n_seq, const uint32_t* deg,

@@ -394,6 +394,14 @@ static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_X = 1024, PW_CUR = 1280;
 static constexpr uint32_t PW_YST = 1280 + 2 * 1024, PW_XST = PW_YST + PD_Y + 1;
 static constexpr uint32_t PW_XCUR = PW_XST + PD_X + 1, PW_YCAP = PW_XCUR + 2 * PD_X;
 static_assert(PW_XCUR % 2 == 0 && PW_YCAP % 2 == 0, "u64 arrays");
+// ...then the fused front pass's y subregions (k_front_fused, FF_GMAX tile groups at most): u64
+// starts (FS_MAX + 1), cursors and ends (FS_MAX each), and the u32 first tile of each subregion
+// in the second pass's tile map (FS_MAX + 1; k_fs_tile_scan).
+static constexpr uint32_t FF_GMAX = 8, FS_MAX = DEGB_NB * FF_GMAX;
+static constexpr uint32_t PW_FST = PW_YCAP + 2 * PD_Y, PW_FCUR = PW_FST + 2 * (FS_MAX + 2),
+                          PW_FCAP = PW_FCUR + 2 * FS_MAX, PW_FTOFF = PW_FCAP + 2 * FS_MAX;
+static_assert(PW_FST % 2 == 0 && PW_FCUR % 2 == 0 && PW_FCAP % 2 == 0, "u64 arrays");
+static_assert(PW_FTOFF + FS_MAX + 1 <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
 // Second-pass records (x, ry): ry's sentinels.
 constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
 constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
@@ -580,16 +588,27 @@ k_degb_scatter(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
 // regions and the fill are all the readers see, so any capacities give the same degrees.
 static constexpr uint32_t FS_STRIDE = 256;
 
+// FF_G (k_front_fused): the groups of tiles whose runs of one region go to a subregion of
+// their own (group = tile % G; see k_front_fused).  The sample counts each group's records
+// apart: block b samples group b % G only (gridDim a multiple of G), sample k lies in sample
+// tile k / SPT (SPT samples per fused tile), so group g's samples are those of tiles g, g + G, ...
+// scnt: G x NB bucket counts, then G x PD_Y digit counts.  G = 1: every FS_STRIDE-th record.
 __global__ void __launch_bounds__(DEGB_THREADS)
 k_front_sample(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mode, int SH,
-               uint32_t NB, int psh, uint32_t* __restrict__ scnt /* NB, then PD_Y */,
-               int xonly /* the fused pass: x endpoints only in the buckets */) {
+               uint32_t NB, int psh, uint32_t* __restrict__ scnt /* G x NB, then G x PD_Y */,
+               int xonly /* the fused pass: x endpoints only in the buckets */, uint32_t G,
+               uint32_t SPT) {
   __shared__ uint32_t hb[DEGB_NB], hy[PD_Y];
   for (uint32_t i = threadIdx.x; i < DEGB_NB; i += DEGB_THREADS) { hb[i] = 0; hy[i] = 0; }
   block_sync();
+  const uint32_t g = blockIdx.x % G, bi = blockIdx.x / G, nbg = gridDim.x / G;
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
-  for (uint64_t k = (uint64_t)blockIdx.x * DEGB_THREADS + threadIdx.x; k < ns;
-       k += (uint64_t)gridDim.x * DEGB_THREADS) {
+  const uint64_t ntl = (ns + SPT - 1) / SPT;                // sample tiles
+  const uint64_t nq = (ntl + G - 1 - g) / G * SPT;          // ... of group g, as samples
+  for (uint64_t q = (uint64_t)bi * DEGB_THREADS + threadIdx.x; q < nq;
+       q += (uint64_t)nbg * DEGB_THREADS) {
+    const uint64_t k = ((q / SPT) * G + g) * SPT + q % SPT;
+    if (k >= ns) continue;
     const uint2 e = uv[k * FS_STRIDE];
     if (e.x >= n_ids || e.y >= n_ids) continue;  // the scatter reports it
     if (!xonly) atomicAdd(&hb[e.x >> SH], 1u);
@@ -598,9 +617,9 @@ k_front_sample(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int fil
   }
   block_sync();
   for (uint32_t i = threadIdx.x; i < NB; i += DEGB_THREADS)
-    if (hb[i]) atomicAdd(&scnt[i], hb[i]);
+    if (hb[i]) atomicAdd(&scnt[g * DEGB_NB + i], hb[i]);
   for (uint32_t i = threadIdx.x; i < PD_Y; i += DEGB_THREADS)
-    if (hy[i]) atomicAdd(&scnt[DEGB_NB + i], hy[i]);
+    if (hy[i]) atomicAdd(&scnt[G * DEGB_NB + g * PD_Y + i], hy[i]);
 }
 
 // Capacity of a region estimated at est items from c samples (est = c * FS_STRIDE): est + 5
@@ -622,17 +641,27 @@ uint64_t fs_room(uint64_t items, uint32_t n_regions) {
 // region ends) within ep_slots u16 entries, and the y-digit regions (ystart: PD_Y + 1 u32,
 // ycur: cursors, ycap: ends) within mid_slots records.  Regions that do not fit get capacity 0
 // (every run then overflows: the caller's exact pass takes over).
+// G > 1 (k_front_fused's tile groups): each region is G subregions s = region * G + group,
+// adjacent in memory, each sized from its group's own samples; every table above is then per
+// subregion (NB * G + 1 starts), and ystart (u32) is not written (nullable).
 __global__ void __launch_bounds__(1024)
 k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_t ep_slots,
              uint64_t mid_slots, unsigned long long* bst, unsigned long long* bcur,
              unsigned long long* bcap, uint32_t* ystart, unsigned long long* ycur,
-             unsigned long long* ycap, unsigned long long* ys64 /* nullable: ystart as u64 */) {
+             unsigned long long* ycap, unsigned long long* ys64 /* nullable: ystart as u64 */,
+             uint32_t G) {
   __shared__ unsigned long long ws[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int pass = 0; pass < 2; ++pass) {
     const uint32_t n = pass ? PD_Y : NB;
     const unsigned long long lim = pass ? m : 2 * m, room = pass ? mid_slots : ep_slots;
-    const unsigned long long c = (uint32_t)t < n ? fs_cap(scnt[(pass ? DEGB_NB : 0) + t], lim) : 0ull;
+    const uint32_t* sc = scnt + (pass ? G * DEGB_NB : 0);
+    unsigned long long cg[8], c = 0;  // (G <= 8)
+#pragma unroll
+    for (uint32_t g = 0; g < 8; ++g) {
+      cg[g] = ((uint32_t)t < n && g < G) ? fs_cap(sc[g * (pass ? PD_Y : DEGB_NB) + t], lim) : 0ull;
+      c += cg[g];
+    }
     unsigned long long incl = c;  // inclusive wave scan (u64)
     for (int o = 1; o < 64; o <<= 1) {
       const unsigned long long v = __shfl_up(incl, o);
@@ -643,25 +672,30 @@ k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_
     unsigned long long add = 0, total = 0;
     for (int i = 0; i < 16; ++i) { if (i < w) add += ws[i]; total += ws[i]; }
     const bool fits = total <= room;
-    const unsigned long long st = fits ? add + incl - c : 0ull, end = fits ? st + c : 0ull;
+    unsigned long long st = fits ? add + incl - c : 0ull;
     if ((uint32_t)t < n) {
-      if (pass) {
-        ystart[t] = (uint32_t)st;
-        if (ys64) ys64[t] = st;
-        ycur[t] = st;
-        ycap[t] = end;
-      } else {
-        bst[t] = st;
-        bcur[t] = st;
-        bcap[t] = end;
+      for (uint32_t g = 0; g < G; ++g) {
+        const unsigned long long end = fits ? st + cg[g] : 0ull;
+        const uint32_t q = t * G + g;
+        if (pass) {
+          if (ystart) ystart[q] = (uint32_t)st;
+          if (ys64) ys64[q] = st;
+          ycur[q] = st;
+          ycap[q] = end;
+        } else {
+          bst[q] = st;
+          bcur[q] = st;
+          bcap[q] = end;
+        }
+        st = end;
       }
     }
     if (t == 0) {
       if (pass) {
-        ystart[n] = (uint32_t)(fits ? total : 0ull);
-        if (ys64) ys64[n] = fits ? total : 0ull;
+        if (ystart) ystart[n * G] = (uint32_t)(fits ? total : 0ull);
+        if (ys64) ys64[n * G] = fits ? total : 0ull;
       }
-      else bst[n] = fits ? total : 0ull;
+      else bst[n * G] = fits ? total : 0ull;
     }
     block_sync();
   }
@@ -752,6 +786,12 @@ k_degb_scatter_cap(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int
 // Tile: FF_NT x FF_IT records.  LDS: the tile staged twice 64 KB (x; digit << 16 | y_lo), the x
 // endpoints restaged into the first half, and the run tables of both sorts.
 static constexpr int FF_NT = 1024, FF_IT = 16;
+// Tile groups (G = FF_G, round 6): every region is G adjacent subregions, and tile t reserves its
+// runs in subregion t % G.  With gridDim a multiple of G, block b's tiles all belong to group
+// b % G, and blocks b, b + 8, ... share an XCD (round-robin dispatch: for speed only, correctness
+// never depends on it).  So consecutive runs of a subregion come from one XCD and meet in its L2,
+// which writes whole lines instead of each XCD writing its own partial lines of a 32-64 B run
+// (the pass wrote 14.9 GB for its 8.6 GB: profiles/r05/ev6/pmc_table.md).
 // Persistent: gridDim blocks (one per CU) walk the tiles blockIdx.x, + gridDim.x, ...  The x runs are
 // staged and written first, then the y runs staged; the next tile's records are loaded right
 // after that (the last use of this tile's records in registers) so that their HBM latency
@@ -767,7 +807,7 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
               unsigned long long* bcur, const unsigned long long* __restrict__ bcap,
               uint16_t* __restrict__ ep, uint32_t* __restrict__ selfc, uint32_t* ovf_y,
               uint32_t* ovf_x, uint32_t* err, uint32_t* __restrict__ xhist, int shx,
-              int xdd /* shx == SH + 2: the x digits come from the x runs */) {
+              int xdd /* shx == SH + 2: the x digits come from the x runs */, uint32_t G) {
   constexpr int TILE = FF_NT * FF_IT;
   __shared__ uint32_t sa[TILE], sb[TILE];
   __shared__ uint32_t ty[DEGB_NB + 1], tx[DEGB_NB + 1], hxd[PD_X], wsum[2 * (FF_NT / 64)];
@@ -788,6 +828,7 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
   uint64_t tile = blockIdx.x;
   load(tile);
   for (; tile < ntiles; tile += gridDim.x) {
+  const uint32_t grp = (uint32_t)(tile % G);  // this tile's subregion of every region
   for (uint32_t i = t; i < DEGB_NB; i += FF_NT) { ty[i] = 0; tx[i] = 0; }
   for (uint32_t i = t; i < PD_X; i += FF_NT) hxd[i] = 0;
   const uint64_t base = tile * TILE;
@@ -825,17 +866,18 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     if (lane == 63) { wsum[w] = i1; wsum[FF_NT / 64 + w] = i2; }
     unsigned long long g1 = 0, g2 = ~0ull;
     if ((uint32_t)t < NB) {
+      const uint32_t q = t * G + grp;  // region t's subregion of this tile's group
       uint32_t fit = 0;
       if (c1) {
-        g1 = atomicAdd(&ycur[t], (unsigned long long)c1);
-        const unsigned long long cap = ycap[t];
+        g1 = atomicAdd(&ycur[q], (unsigned long long)c1);
+        const unsigned long long cap = ycap[q];
         fit = g1 + c1 <= cap ? c1 : g1 < cap ? (uint32_t)(cap - g1) : 0u;
         if (fit < c1) atomicOr(ovf_y, 1u);
       }
       yfit[t] = fit;
       if (c2) {
-        g2 = atomicAdd(&bcur[t], (unsigned long long)c2);
-        if (g2 + c2 > bcap[t]) {
+        g2 = atomicAdd(&bcur[q], (unsigned long long)c2);
+        if (g2 + c2 > bcap[q]) {
           atomicOr(ovf_x, 1u);
           g2 = ~0ull;
         }
@@ -902,7 +944,8 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
             const unsigned long long* __restrict__ bstart2 = nullptr,
             const uint64_t* __restrict__ rec0 = nullptr,
             const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */,
-            const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */) {
+            const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */,
+            uint32_t G = 1) {
   // span words of dynamic LDS (degb_hist_lds): 16 KB for R-MAT-22's 4096-id buckets, where a
   // fixed 128 KB array held the CU to one block
   extern __shared__ uint32_t cnt[];
@@ -912,17 +955,20 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
   block_sync();
   const int lane = threadIdx.x & 63;
   // ep2 (nullable, tile-major bstart2): a second endpoint array (the fused front half's x ids)
-  for (int sg = 0; sg < (ep2 ? 2 : 1); ++sg) {
+  // G > 1 (with bstart): the bucket's entries lie in G subregions (k_front_fused's groups)
+  for (uint32_t sq = 0; sq < (ep2 ? 2u : 1u) * G; ++sq) {
+  const int sg = (int)(sq / G);
+  const uint32_t bq = b * G + sq % G;  // the bucket's subregion (G = 1: the bucket)
   const uint16_t* __restrict__ ep_s = sg ? ep2 : ep;
   // bstart (tile-major counts): bucket starts and the total; else the digit-major offsets
   const uint64_t last = (uint64_t)NB * nchunks - 1;
-  uint64_t s0 = sg ? bstart2[b] : bstart ? bstart[b] : offsets[(uint64_t)b * nchunks];
-  uint64_t s1 = sg ? bstart2[b + 1]
-                   : bstart ? bstart[b + 1]
+  uint64_t s0 = sg ? bstart2[bq] : bstart ? bstart[bq] : offsets[(uint64_t)b * nchunks];
+  uint64_t s1 = sg ? bstart2[bq + 1]
+                   : bstart ? bstart[bq + 1]
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
-  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[b]);  // (a region's fill past its end: dropped)
-  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[b]);
+  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[bq]);  // (a region's fill past its end: dropped)
+  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[bq]);
   if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
     const uint32_t lm = (1u << SH) - 1u;
     for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
@@ -1133,13 +1179,16 @@ __device__ __forceinline__ void hist16s_slices(const unsigned long long* __restr
                                                const unsigned long long* __restrict__ ys,
                                                const unsigned long long* __restrict__ yf,
                                                uint32_t NB, uint64_t CH, uint32_t* wsum,
-                                               uint32_t& ns, uint32_t& p0) {
+                                               uint32_t& ns, uint32_t& p0, uint32_t G) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   ns = 0;
   if ((uint32_t)t < NB) {
-    const uint64_t nx = min(xs[t + 1], xf[t]) - min(xs[t], min(xs[t + 1], xf[t]));
-    const uint64_t ny = min(ys[t + 1], yf[t]) - min(ys[t], min(ys[t + 1], yf[t]));
-    ns = (uint32_t)max((uint64_t)1, (nx + ny + CH - 1) / CH);
+    uint64_t n = 0;
+    for (uint32_t q = t * G; q < (t + 1) * G; ++q) {  // the bucket's G subregions
+      n += min(xs[q + 1], xf[q]) - min(xs[q], min(xs[q + 1], xf[q]));
+      n += min(ys[q + 1], yf[q]) - min(ys[q], min(ys[q + 1], yf[q]));
+    }
+    ns = (uint32_t)max((uint64_t)1, (n + CH - 1) / CH);
   }
   const uint32_t incl = wave_incl_scan(ns);
   if (lane == 63) wsum[w] = incl;
@@ -1155,14 +1204,15 @@ __global__ void __launch_bounds__(DEGB_THREADS)
 k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __restrict__ xs,
                const unsigned long long* __restrict__ xf, const uint16_t* __restrict__ ey,
                const unsigned long long* __restrict__ ys, const unsigned long long* __restrict__ yf,
-               uint32_t NB, uint32_t n_ids, uint64_t CH, uint32_t* __restrict__ deg) {
+               uint32_t NB, uint32_t n_ids, uint64_t CH, uint32_t* __restrict__ deg,
+               uint32_t G /* subregions per bucket (k_front_fused's groups) */) {
   __shared__ uint32_t pk[32768];
   __shared__ uint32_t wsum[DEGB_THREADS / 64], s_b, s_s, s_n;
   const int t = threadIdx.x;
   // slice table: thread t = bucket t
   if (t == 0) s_b = INV;
   uint32_t ns, p0;
-  hist16s_slices(xs, xf, ys, yf, NB, CH, wsum, ns, p0);
+  hist16s_slices(xs, xf, ys, yf, NB, CH, wsum, ns, p0, G);
   if ((uint32_t)t < NB && blockIdx.x >= p0 && blockIdx.x < p0 + ns) {
     s_b = t;
     s_s = blockIdx.x - p0;
@@ -1172,9 +1222,12 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
   const uint32_t b = s_b;
   if (b == INV) return;  // (uniform: past the last slice)
   const uint32_t sl = s_s, nsl = s_n;
-  const uint64_t x0 = xs[b], x1 = max(x0, min(xs[b + 1], xf[b]));
-  const uint64_t y0 = ys[b], y1 = max(y0, min(ys[b + 1], yf[b]));
-  const uint64_t v0 = (uint64_t)sl * CH, v1 = min(v0 + CH, (x1 - x0) + (y1 - y0));
+  // the slice [v0, v1) of the bucket's entries: its x subregions, then its y subregions, as one
+  // sequence (vend: its length)
+  uint64_t vend = 0;
+  for (uint32_t q = b * G; q < (b + 1) * G; ++q)
+    vend += (max(xs[q], min(xs[q + 1], xf[q])) - xs[q]) + (max(ys[q], min(ys[q + 1], yf[q])) - ys[q]);
+  const uint64_t v0 = (uint64_t)sl * CH, v1 = min(v0 + CH, vend);
   // Rounds of RW = 65528 entries (8191 16-B loads: thread 1023 skips its eighth, so a round
   // counts at most 65528 < 65536 of one id into a u16 half) from the 8-aligned entry below the
   // segment's start, in two halves of four loads per thread.  The next round's first half is
@@ -1189,12 +1242,18 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
   for (int k = 0; k < 32; ++k) { lo[k] = 0; hi[k] = 0; }
   for (uint32_t i = t; i < 32768; i += DEGB_THREADS) pk[i] = 0;
   block_sync();
-  for (int sg = 0; sg < 2; ++sg) {
-    const uint64_t off = sg ? (x1 - x0) : 0, len = sg ? (y1 - y0) : (x1 - x0);
+  uint64_t off = 0;
+  for (uint32_t sq = 0; sq < 2 * G; ++sq) {
+    const int sg = (int)(sq / G);
+    const uint32_t bq = b * G + sq % G;
+    const unsigned long long* __restrict__ st = sg ? ys : xs;
+    const unsigned long long* __restrict__ fl = sg ? yf : xf;
+    const uint64_t z0 = st[bq], len = max(z0, min(st[bq + 1], fl[bq])) - z0;
     const uint64_t a = min(max(v0, off), off + len) - off, e = min(max(v1, off), off + len) - off;
+    off += len;
     if (a >= e) continue;  // (uniform)
     const uint16_t* __restrict__ src = sg ? ey : ex;
-    const uint64_t s0 = (sg ? y0 : x0) + a, s1 = (sg ? y0 : x0) + e;
+    const uint64_t s0 = z0 + a, s1 = z0 + e;
     const uint64_t A = s0 & ~7ull, last = (s1 - 1) & ~7ull;
     const uint64_t nr = (s1 - A + RW - 1) / RW;
     uint4 q[4];
@@ -1367,9 +1426,12 @@ size_t degs_tmp_words(uint64_t m, uint32_t n_ids) {
   int SH = 0;
   uint32_t NB = 0;
   if (!degb_params(n_ids, &SH, &NB)) return 1;
-  // samples (2 x 1024), bucket starts / cursors / ends (u64), the u16 entries (+16-B pad)
-  // (+ the fused pass's u64 y starts: its x-only entries need half the room)
-  return 2 * DEGB_NB + 2 * (4 * (size_t)DEGB_NB + 3) + (degs_ep_slots(m, NB) + 1) / 2 + 16;
+  // samples (2 x FS_MAX), bucket starts / cursors / ends (u64, FS_MAX + 1 each), the u16 entries
+  // (+16-B pad): laid out for the fused pass's subregions (FF_GMAX tile groups), which holds
+  // launch_degree_sampled's smaller tables too; the fused pass's x-only entries need at most
+  // fs_room(m, FS_MAX) slots, the sampled pass's both endpoints degs_ep_slots
+  const uint64_t ep = std::max<uint64_t>(degs_ep_slots(m, NB), fs_room(m, FS_MAX));
+  return 2 * FS_MAX + 2 * 3 * ((size_t)FS_MAX + 1) + (ep + 1) / 2 + 16;
 }
 
 bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
@@ -1391,11 +1453,11 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
   const unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
   hipLaunchKernelGGL(k_front_sample, dim3(sg), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m, n_ids,
-                     file_mode, SH, NB, psh, scnt, 0);
+                     file_mode, SH, NB, psh, scnt, 0, 1u, 1u);
   hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
                      degs_ep_slots(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST,
                      (unsigned long long*)(part_ws + PW_CUR), (unsigned long long*)(part_ws + PW_YCAP),
-                     (unsigned long long*)nullptr);
+                     (unsigned long long*)nullptr, 1u);
   if (caps_done) (void)hipEventRecord(caps_done, s);
   const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   hipLaunchKernelGGL(k_degb_scatter_cap, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
@@ -1429,53 +1491,69 @@ bool front_fused_ok(uint64_t m, uint32_t n_ids) {
 
 // the histogram's slice length: about 2m / 1024 entries (at least 2^20), 4 slices per CU
 static uint64_t hist16s_ch(uint64_t m) { return std::max<uint64_t>(1ull << 20, (2 * m + 1023) / 1024); }
+// The packed first-pass records' slots (mid_slots) with G tile groups: the capacities of the
+// NB * G subregions sum to at most this (fs_room), a multiple of 8.
+uint64_t front_fused_slots(uint64_t m, uint32_t n_ids, uint32_t G) {
+  int SH;
+  uint32_t NB;
+  if (!degb_params(n_ids, &SH, &NB)) NB = DEGB_NB;
+  return (fs_room(m, NB * std::max<uint32_t>(1, std::min(G, FF_GMAX))) + 7) & ~7ull;
+}
+
 bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
                         uint32_t* deg, uint32_t* selfc, uint32_t* err, uint32_t* tmp,
                         uint32_t* part_ws, uint64_t* mid, uint64_t mid_slots, uint32_t* stats,
                         uint32_t* ovf_x, uint32_t* ovf_y, hipStream_t s,
-                        void (*mark)(void*, const char*), void* mark_arg) {
+                        void (*mark)(void*, const char*), void* mark_arg, uint32_t G) {
   int SH;
   uint32_t NB;
   if (!front_fused_ok(m, n_ids) || mid_slots % 8 != 0) return false;
   degb_params(n_ids, &SH, &NB);
+  G = std::max<uint32_t>(1, std::min(G, FF_GMAX));
+  const unsigned nt = (unsigned)((m + FF_NT * FF_IT - 1) / (FF_NT * FF_IT));
+  // persistent grid, one block per CU; with G groups a multiple of G (block b's tiles are then
+  // all of group b % G)
+  unsigned grid = std::min(nt, device_cus());
+  if (G > 1 && grid >= G) grid -= grid % G;
   uint32_t* scnt = tmp;
-  unsigned long long* bst = (unsigned long long*)(tmp + 2 * DEGB_NB);
-  unsigned long long* bcur = bst + DEGB_NB + 1;
-  unsigned long long* bcap = bcur + DEGB_NB;
-  unsigned long long* ys64 = bcap + DEGB_NB + 1;
-  uint16_t* ep = (uint16_t*)(((uintptr_t)(ys64 + DEGB_NB + 1) + 15) & ~(uintptr_t)15);
+  unsigned long long* bst = (unsigned long long*)(tmp + 2 * FS_MAX);
+  unsigned long long* bcur = bst + FS_MAX + 1;
+  unsigned long long* bcap = bcur + FS_MAX + 1;
+  uint16_t* ep = (uint16_t*)(((uintptr_t)(bcap + FS_MAX + 1) + 15) & ~(uintptr_t)15);
+  unsigned long long* ys64 = (unsigned long long*)(part_ws + PW_FST);
+  unsigned long long* ycur = (unsigned long long*)(part_ws + PW_FCUR);
+  unsigned long long* ycap = (unsigned long long*)(part_ws + PW_FCAP);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
-  (void)hipMemsetAsync(scnt, 0, 2 * DEGB_NB * 4, s);
+  (void)hipMemsetAsync(scnt, 0, 2 * G * DEGB_NB * 4, s);
   (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
-  const unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
+  unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
+  sg = (sg + G - 1) / G * G;
   hipLaunchKernelGGL(k_front_sample, dim3(sg), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m, n_ids,
-                     file_mode, SH, NB, SH, scnt, 1);
-  unsigned long long* ycur = (unsigned long long*)(part_ws + PW_CUR);
-  unsigned long long* ycap = (unsigned long long*)(part_ws + PW_YCAP);
+                     file_mode, SH, NB, SH, scnt, 1, G, (uint32_t)(FF_NT * FF_IT / FS_STRIDE));
   hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
-                     fs_room(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST, ycur, ycap, ys64);
+                     fs_room(m, NB * G), mid_slots, bst, bcur, bcap, (uint32_t*)nullptr, ycur, ycap,
+                     ys64, G);
   if (mark) mark(mark_arg, "degree_sample");
   uint32_t* oa = (uint32_t*)mid;
   uint16_t* ob = (uint16_t*)(oa + mid_slots);
-  const unsigned nt = (unsigned)((m + FF_NT * FF_IT - 1) / (FF_NT * FF_IT));
-  hipLaunchKernelGGL(k_front_fused, dim3(std::min(nt, device_cus())), dim3(FF_NT), 0, s,
+  hipLaunchKernelGGL(k_front_fused, dim3(grid), dim3(FF_NT), 0, s,
                      (const uint2*)uv, m, n_ids,
                      file_mode, SH, NB, oa, ob, ycur, (const unsigned long long*)ycap, bcur,
                      (const unsigned long long*)bcap, ep, selfc, ovf_y, ovf_x, err,
                      part_ws + PW_X, part_shift(n_ids, PD_X),
-                     (int)(part_shift(n_ids, PD_X) == SH + 2));
+                     (int)(part_shift(n_ids, PD_X) == SH + 2), G);
   if (mark) mark(mark_arg, "front_fused");
   // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
   if (SH > 15) {
     const uint64_t CH = hist16s_ch(m);
-    const unsigned grid = (unsigned)(NB + (2 * m + CH - 1) / CH + 1);
+    const unsigned hgrid = (unsigned)(NB + (2 * m + CH - 1) / CH + 1);
     (void)hipMemsetAsync(deg, 0, (size_t)n_ids * 4, s);
-    hipLaunchKernelGGL(k_degb_hist16s, dim3(grid), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
+    hipLaunchKernelGGL(k_degb_hist16s, dim3(hgrid), dim3(DEGB_THREADS), 0, s, (const uint16_t*)ep,
                        (const unsigned long long*)bst, (const unsigned long long*)bcur,
                        (const uint16_t*)ob, (const unsigned long long*)ys64,
-                       (const unsigned long long*)ycur, NB, n_ids, CH, deg);
+                       (const unsigned long long*)ycur, NB, n_ids, CH, deg, G);
     if (stats) launch_deg_stats(deg, n_ids, stats, s);
   } else
     hipLaunchKernelGGL(k_degb_hist, dim3(NB), dim3(DEGB_THREADS), degb_hist_lds(SH, 1), s, (const uint16_t*)ep,
@@ -1483,7 +1561,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)ob, (const unsigned long long*)ys64,
                        (const uint64_t*)nullptr, (const unsigned long long*)bcur,
-                       (const unsigned long long*)ycur);
+                       (const unsigned long long*)ycur, G);
   return true;
 }
 
@@ -2788,6 +2866,67 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32
   hist[t] = 0;
 }
 
+// The second pass's tile map over the fused front pass's y subregions (k_front_fused): the
+// filled part of subregion q, [st[q], min(cur[q], cap[q])), is cut into tiles of TILE records,
+// so that no tile crosses a subregion (the unwritten slack between subregions is never read,
+// and a tile's y digit is its subregion's, q / G).  k_fs_tile_scan (one block): toff[q] = the
+// first tile of subregion q, toff[S] = the tiles.  k_fs_tile_desc (one thread per tile slot of
+// the launch, nt of them): desc[j] = (first position, digit << 16 | records), records 0 past
+// the last tile.
+__global__ void __launch_bounds__(1024)
+k_fs_tile_scan(const unsigned long long* __restrict__ st, const unsigned long long* __restrict__ cur,
+               const unsigned long long* __restrict__ cap, uint32_t S, uint32_t TILE,
+               uint32_t* __restrict__ toff) {
+  __shared__ uint32_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  constexpr uint32_t PER = FS_MAX / 1024;  // subregions per thread
+  uint32_t nt[PER], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    const uint32_t q = t * PER + i;
+    nt[i] = 0;
+    if (q < S) {
+      const unsigned long long f = min(cur[q], cap[q]);
+      const uint64_t n = f > st[q] ? f - st[q] : 0;
+      nt[i] = (uint32_t)((n + TILE - 1) / TILE);
+    }
+    sum += nt[i];
+  }
+  const uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63) wsum[w] = incl;
+  block_sync();
+  uint32_t run = incl - sum, tot = 0;
+  for (int i = 0; i < 16; ++i) { if (i < w) run += wsum[i]; tot += wsum[i]; }
+#pragma unroll
+  for (uint32_t i = 0; i < PER; ++i) {
+    const uint32_t q = t * PER + i;
+    if (q < S) toff[q] = run;
+    run += nt[i];
+  }
+  if (t == 0) toff[S] = tot;
+}
+
+__global__ void __launch_bounds__(256)
+k_fs_tile_desc(const unsigned long long* __restrict__ st, const unsigned long long* __restrict__ cur,
+               const unsigned long long* __restrict__ cap, const uint32_t* __restrict__ toff,
+               uint32_t S, uint32_t G, uint32_t TILE, uint64_t nt, uint2* __restrict__ desc) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nt) return;
+  if (j >= toff[S]) {
+    desc[j] = make_uint2(0u, 0u);
+    return;
+  }
+  uint32_t lo = 0, cnt = S;  // the last q with toff[q] <= j (toff[0] = 0)
+  while (cnt > 0) {
+    const uint32_t h = cnt >> 1;
+    if (toff[lo + h] <= (uint32_t)j) { lo += h + 1; cnt -= h + 1; } else cnt = h;
+  }
+  const uint32_t q = lo - 1;
+  const uint64_t k = j - toff[q], p0 = st[q] + k * TILE, f = min(cur[q], cap[q]);
+  const uint32_t n = (uint32_t)min((uint64_t)TILE, f - p0);
+  desc[j] = make_uint2((uint32_t)p0, ((q / G) << 16) | n);
+}
+
 // ND: digits of this pass (PD_Y for MODE 0, PD_X for MODE 1), ND / NT per thread in the scan.
 // MODE 0 also counts the x digits (PD_X) of the second pass into xhist.
 // in, m: the input and its positions.  REG (MODE 1): the input lies in the first pass's
@@ -2805,7 +2944,8 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
        const uint32_t* __restrict__ rank, uint32_t n_rank, int ysh,
        const uint32_t* __restrict__ in_starts, int ish,
        const unsigned long long* __restrict__ in_fill, const unsigned long long* __restrict__ in_cap,
-       const unsigned long long* __restrict__ cap_end, uint32_t* ovf) {
+       const unsigned long long* __restrict__ cap_end, uint32_t* ovf,
+       const uint2* __restrict__ tdesc = nullptr /* IN6: the tile map (k_fs_tile_desc) */) {
   static_assert(ND % NT == 0 || NT % ND == 0, "digits per thread");
   static_assert(!REG || MODE == 1, "capacity-region input: the second pass only");
   static_assert(!OUT6 || MODE == 1, "packed output: the second pass only");
@@ -2818,33 +2958,53 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[ND], tstart[ND], hx[MODE == 0 ? PD_X : 1], wsum[NT / 64];
   __shared__ unsigned long long gbase[ND], gcap[MODE == 0 ? ND : 1];
-  __shared__ uint32_t sst[RG ? PD_Y + 2 : 1], sfill[RG ? PD_Y : 1], s_nv;
+  __shared__ uint32_t sst[RG && !IN6 ? PD_Y + 2 : 1], sfill[RG && !IN6 ? PD_Y : 1], s_nv;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
-  const uint64_t lim = RG ? min(m, (uint64_t)in_starts[PD_Y]) : m;
-  if (tbase >= lim) return;  // (the grid covers m slots; the regions may end earlier)
-  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, lim - tbase);
+  uint64_t tbase;
+  uint32_t tile_n, tdig = 0;
+  if constexpr (IN6) {  // one subregion's tile: (first position, y digit << 16 | records)
+    const uint2 dsc = tdesc[blockIdx.x];
+    tbase = dsc.x;
+    tile_n = dsc.y & 0xFFFFu;
+    tdig = dsc.y >> 16;
+    if (tile_n == 0) return;  // (the grid covers the largest tile count)
+  } else {
+    tbase = (uint64_t)blockIdx.x * TILE;
+    const uint64_t lim = RG ? min(m, (uint64_t)in_starts[PD_Y]) : m;
+    if (tbase >= lim) return;  // (the grid covers m slots; the regions may end earlier)
+    tile_n = (uint32_t)min((uint64_t)TILE, lim - tbase);
+  }
   for (uint32_t i = t; i < ND; i += NT) hist[i] = 0;
   if (MODE == 0)
     for (uint32_t i = t; i < PD_X; i += NT) hx[i] = 0;
   uint64_t rec[PT_ITEMS];
   uint32_t li[PT_ITEMS];
   uint32_t vm = 0;  // bit k: item k is a record
-  if constexpr (REG) {
-    // IN6: the fused front pass's packed records (k_front_fused): x from the u32 array, y's low
-    // bits from the u16 array after it (m positions each), y's digit from the region
+  if constexpr (IN6) {
+    // the fused front pass's packed records (k_front_fused): x from the u32 array, y's low bits
+    // from the u16 array after it (m positions each), y's digit from the tile's subregion
     const uint32_t* ia = (const uint32_t*)in;
     const uint16_t* ib = (const uint16_t*)(ia + m);
-    uint16_t yb[IN6 ? PT_ITEMS : 1];
+    uint16_t yb[PT_ITEMS];
 #pragma unroll
     for (int k = 0; k < PT_ITEMS; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
-      if (IN6) {
-        rec[k] = j < tile_n ? ia[tbase + j] : 0u;
-        yb[k] = j < tile_n ? ib[tbase + j] : (uint16_t)0;
-      } else {
-        rec[k] = j < tile_n ? in[tbase + j] : 0ull;
-      }
+      rec[k] = j < tile_n ? ia[tbase + j] : 0u;
+      yb[k] = j < tile_n ? ib[tbase + j] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      vm |= (uint32_t)(j < tile_n) << k;
+      rec[k] |= (uint64_t)((tdig << ish) | yb[k]) << 32;
+    }
+  } else if constexpr (REG) {
+    // the first pass's capacity regions (launch_part_first_caps): y's digit from the region
+    // starts, positions past a region's fill masked
+#pragma unroll
+    for (int k = 0; k < PT_ITEMS; ++k) {
+      const uint32_t j = (uint32_t)k * NT + t;
+      rec[k] = j < tile_n ? in[tbase + j] : 0ull;
     }
     tile_regions<PD_Y>(in_starts, tbase, tile_n, sst);  // (the loads above are in flight)
     const uint32_t d0 = sst[0];
@@ -2859,7 +3019,6 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
       const uint64_t pos = tbase + min(j, tile_n - 1);
       const uint32_t d = tile_digit(sst, pos);
       vm |= (uint32_t)(j < tile_n && pos < sfill[d - d0]) << k;
-      if (IN6) rec[k] |= (uint64_t)((d << ish) | yb[k]) << 32;
     }
   } else {
 #pragma unroll
@@ -3042,26 +3201,50 @@ void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uin
 // packed.
 void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, uint32_t n_rank,
                         uint64_t* pre, uint32_t* ws, hipStream_t s, bool out6, uint64_t mid_slots,
-                        bool caps, bool in6) {
+                        bool caps, bool in6, uint32_t G) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   const int ysh = std::max(sh - 8, 0);
   uint32_t* xhist = ws + PW_X;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
   hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
+  constexpr uint32_t TILE = PT1_THREADS * PT1_ITEMS;
+  if (caps && in6) {
+    // the fused pass's subregions (launch_front_fused: ws's PW_F* tables, G per y digit): the
+    // tile map, its descriptors in the spare 2 B per slot behind the packed records
+    int SH;
+    uint32_t NB;
+    if (!degb_params(n_rank, &SH, &NB)) NB = DEGB_NB;
+    G = std::max<uint32_t>(1, std::min(G, FF_GMAX));
+    const uint32_t S = NB * G;
+    const unsigned long long* fst = (const unsigned long long*)(ws + PW_FST);
+    const unsigned long long* fcur = (const unsigned long long*)(ws + PW_FCUR);
+    const unsigned long long* fcap = (const unsigned long long*)(ws + PW_FCAP);
+    uint32_t* toff = ws + PW_FTOFF;
+    const uint64_t nt = mid_slots / TILE + S + 1;  // >= the tiles (one partial tile per subregion)
+    uint2* desc = (uint2*)((char*)mid + 6 * mid_slots);  // (mid holds 8 B per slot)
+    hipLaunchKernelGGL(k_fs_tile_scan, dim3(1), dim3(1024), 0, s, fst, fcur, fcap, S, TILE, toff);
+    hipLaunchKernelGGL(k_fs_tile_desc, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, fst, fcur,
+                       fcap, (const uint32_t*)toff, S, G, TILE, nt, desc);
+    auto k = out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true, true>
+                  : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true, true>;
+    hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, mid_slots, pre, m, cursor,
+                       xhist, shx, shx, rank, n_rank, ysh, (const uint32_t*)nullptr, sh,
+                       (const unsigned long long*)nullptr, (const unsigned long long*)nullptr,
+                       (const unsigned long long*)nullptr, (uint32_t*)nullptr, (const uint2*)desc);
+    return;
+  }
   const uint64_t pos = caps && mid_slots ? mid_slots : m;
-  uint64_t nt = (pos + PT1_THREADS * PT1_ITEMS - 1) / (PT1_THREADS * PT1_ITEMS);
-  auto k = caps ? (in6 ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true, true>
-                               : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true, true>)
-                       : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
-                               : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>))
+  uint64_t nt = (pos + TILE - 1) / TILE;
+  auto k = caps ? (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true, true>
+                        : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false, true>)
                 : (out6 ? k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, true>
                         : k_part<1, PT1_THREADS, PT1_ITEMS, PD_X, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(PT1_THREADS), 0, s, mid, pos, pre, m, cursor, xhist,
                      shx, shx, rank, n_rank, ysh, (const uint32_t*)(ws + PW_YST), sh,
                      (const unsigned long long*)(ws + PW_CUR),
                      caps ? (const unsigned long long*)(ws + PW_YCAP) : (const unsigned long long*)nullptr,
-                     (const unsigned long long*)nullptr, (uint32_t*)nullptr);
+                     (const unsigned long long*)nullptr, (uint32_t*)nullptr, (const uint2*)nullptr);
 }
 
 void launch_part_gather(const uint32_t* uv, uint64_t m, const uint32_t* rank, uint32_t n_rank,

@@ -158,17 +158,19 @@ def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env)
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
-@pytest.mark.parametrize("mode,ov", [(0, 4), (1, 4), (0, 2), (1, 2)])
-def test_graph2tree_dev_sampled_capacities(oracle, gpu, options, mode, ov):
+@pytest.mark.parametrize("mode,ov,ff", [(0, 4, 8), (1, 4, 8), (0, 4, 1), (1, 4, 3), (0, 2, 8),
+                                        (1, 2, 8)])
+def test_graph2tree_dev_sampled_capacities(oracle, gpu, options, mode, ov, ff):
     """From 2^25 records the front half writes into capacity regions sized from a 1/256 sample
     of the records (no counting read): one fused read for the degrees and the packed first
-    partition (part_overlap 4, k_front_fused), or the degree scatter beside the first
-    partition pass (2).  R-MAT 21 (2^25 records), seq / parent / pst bit-exact in both degree
-    conventions, the exact pass not needed."""
+    partition (part_overlap 4, k_front_fused; ff tile groups, each with its own subregion of
+    every region, read back through the second pass's tile map), or the degree scatter beside
+    the first partition pass (2).  R-MAT 21 (2^25 records), seq / parent / pst bit-exact in
+    both degree conventions, the exact pass not needed."""
     import torch
     from sheep_amd import capi, device
 
-    options(part_overlap=ov)
+    options(part_overlap=ov, ff_groups=ff)
     uv_d = device.rmat(21, 16, 77 + mode)
     s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << 21, mode)
     torch.cuda.synchronize()
@@ -177,6 +179,30 @@ def test_graph2tree_dev_sampled_capacities(oracle, gpu, options, mode, ov):
     assert ("front_fused" in t) == (ov == 4)
     uv = uv_d.cpu().numpy().view(np.uint32)
     seq = oracle.degree_sequence(uv, mode)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
+@pytest.mark.parametrize("ff", [8, 1])
+def test_graph2tree_dev_fused_groups_sorted_stream(oracle, gpu, options, ff):
+    """The fused pass's tile groups on a stream sorted by tail (an adjacency-ordered file): each
+    group's records of a region then come from a few tiles, so the subregions' sizes follow the
+    order, not the shares of a shuffled stream.  The per-group sample sees the same order;
+    whatever it misjudges goes through the overflow paths.  R-MAT 21 sorted by (tail, head),
+    bit-exact."""
+    import torch
+    from sheep_amd import device
+
+    options(ff_groups=ff)
+    uv = device.rmat(21, 16, 91).cpu().numpy().view(np.uint32)
+    uv = uv[np.lexsort((uv[:, 1], uv[:, 0]))]
+    uv_d = torch.from_numpy(np.ascontiguousarray(uv).view(np.int32)).cuda().view(torch.uint32)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, 1 << 21)
+    torch.cuda.synchronize()
+    seq = oracle.degree_sequence(uv)
     p, w = oracle.build_tree(uv, seq)
     assert n == len(seq)
     assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
