@@ -1726,12 +1726,13 @@ static uint32_t multi_tree(Ctx& c, Comm& comm, const uint32_t* d_uv, uint64_t m,
                        stats, ovf_deg, c.d_err + 3, s, nullptr, nullptr, ff_groups());
     HIP_CHECK(hipEventRecord(c.part_ev[1], s));
     part_done = c.part_ev[1];
-    // this shard's degrees are complete unless an x bucket outgrew its region (a local
-    // decision: the exact pass has no collectives)
-    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 4, hipMemcpyDeviceToHost, s));
+    // this shard's degrees are complete unless a region outgrew its capacity — an x bucket, or
+    // a y digit, whose ids the histogram counts from the packed records (a local decision: the
+    // exact pass has no collectives)
+    HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, ovf_deg, 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (tm) tm->mark("front_fused");
-    if (c.h_pinned[4]) {
+    if (c.h_pinned[4] || c.h_pinned[5]) {
       degree_dev(c, d_uv, m, n_ids, mode, deg_local, selfc, s);
       if (tm) tm->mark("degree_exact");
     }
@@ -2126,15 +2127,16 @@ int sheep_graph2tree_dev(const uint32_t* d_uv, uint64_t m, uint32_t n_ids, int d
     tm.mark("degree_hist");
     HIP_CHECK(hipEventRecord(c.part_ev[1], s));
     // One readback: the error word and both overflow words (d_err[0..3]) with the degree stats.
-    // The degrees are complete unless an x bucket outgrew its region; an id out of range leaves
-    // the pass's record array short, which is reported here, before anything reads it (the
-    // check_err the sequence would otherwise need).
+    // The degrees are complete unless a region outgrew its capacity: an x bucket, or a y digit
+    // (the histogram counts y's ids from the packed records, which then lost the run's tail);
+    // an id out of range leaves the pass's record array short, which is reported here, before
+    // anything reads it (the check_err the sequence would otherwise need).
     HIP_CHECK(hipMemcpyAsync(c.h_pinned + 4, c.d_err, 16, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(c.h_pinned, stats, 12, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (c.h_pinned[4] & ERR_RANGE) check_err(c, s);  // (throws -ERANGE, resetting the word)
     stats_host = true;
-    if (c.h_pinned[6]) {
+    if (c.h_pinned[6] || c.h_pinned[7]) {
       degree_dev(c, d_uv, m, n_ids, degree_mode, deg, selfc, s, false, nullptr, stats);
       tm.mark("degree_exact");
       stats_host = false;  // (the exact pass rewrote them)

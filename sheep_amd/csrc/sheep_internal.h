@@ -226,7 +226,7 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
 // The fused front pass (sheep_kernels.hip k_front_fused): degrees and the first partition from
 // ONE read of the records, into sampled capacity regions (mid_slots, a multiple of 8, packed
 // records in mid).  *ovf_x: the degrees need the exact pass; *ovf_y: the partition must be
-// redone from uv.  False when not applicable (front_fused_ok).
+// redone from uv, and the degrees too (the histogram counts y's ids from the packed records).  False when not applicable (front_fused_ok).
 // G (option ff_groups, 1..8): tile groups, each writing its own subregion of every region
 // (sheep_kernels.hip k_front_fused); front_fused_slots: the mid_slots these regions need.
 bool front_fused_ok(uint64_t m, uint32_t n_ids);

@@ -1481,7 +1481,8 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
 // partition's packed records in mid (mid_slots positions: u32 x array, then u16 y_lo array) and
 // its region tables in part_ws (PW_YST / PW_CUR / PW_YCAP, the x digits at PW_X).  tmp:
 // degs_tmp_words.  ovf_x: an x bucket outgrew its region (the degrees are then incomplete: the
-// caller runs the exact pass); ovf_y: a y region (the caller partitions again from uv).
+// caller runs the exact pass); ovf_y: a y region (the histogram's y ids are then incomplete too:
+// the caller runs the exact pass, and partitions again from uv).
 bool front_fused_ok(uint64_t m, uint32_t n_ids) {
   int SH;
   uint32_t NB;
@@ -1492,12 +1493,11 @@ bool front_fused_ok(uint64_t m, uint32_t n_ids) {
 // the histogram's slice length: about 2m / 1024 entries (at least 2^20), 4 slices per CU
 static uint64_t hist16s_ch(uint64_t m) { return std::max<uint64_t>(1ull << 20, (2 * m + 1023) / 1024); }
 // The packed first-pass records' slots (mid_slots) with G tile groups: the capacities of the
-// NB * G subregions sum to at most this (fs_room), a multiple of 8.
+// PD_Y * G y subregions (k_front_caps sizes every digit, used or not) sum to at most this
+// (fs_room), a multiple of 8.
 uint64_t front_fused_slots(uint64_t m, uint32_t n_ids, uint32_t G) {
-  int SH;
-  uint32_t NB;
-  if (!degb_params(n_ids, &SH, &NB)) NB = DEGB_NB;
-  return (fs_room(m, NB * std::max<uint32_t>(1, std::min(G, FF_GMAX))) + 7) & ~7ull;
+  (void)n_ids;
+  return (fs_room(m, PD_Y * std::max<uint32_t>(1, std::min(G, FF_GMAX))) + 7) & ~7ull;
 }
 
 bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,

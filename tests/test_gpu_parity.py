@@ -236,6 +236,35 @@ def test_graph2tree_dev_sampled_capacities_overflow(oracle, gpu, options, ov):
     assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
 
 
+@pytest.mark.parametrize("ff", [8, 1])
+def test_graph2tree_dev_fused_y_overflow_only(oracle, gpu, options, ff):
+    """Only the y regions overflow: every 256th record (the sampled ones) has a uniform head, the
+    others a head in one y digit's 1024 ids, while the tails stay uniform (the x buckets fit).
+    The fused pass's histogram counts the heads from the packed records, so a dropped y run
+    loses degrees too: the exact degree pass must run on the y flag alone (round 6; it ran on the
+    x flag only).  Bit-exact."""
+    import torch
+    from sheep_amd import capi, device
+
+    options(ff_groups=ff)
+    m, n_ids = 1 << 25, 1 << 20
+    rng = np.random.default_rng(21)
+    uv = rng.integers(0, n_ids, size=(m, 2), dtype=np.uint32)
+    keep = np.zeros(m, bool)
+    keep[::256] = True
+    uv[~keep, 1] = rng.integers(5 << 10, 6 << 10, size=int((~keep).sum()), dtype=np.uint32)
+    uv_d = torch.from_numpy(uv.view(np.int32)).cuda().view(torch.uint32)
+    s_d, p_d, w_d, n = device.graph2tree(uv_d, n_ids)
+    torch.cuda.synchronize()
+    assert "degree_exact" in dict(capi.last_timings())
+    seq = oracle.degree_sequence(uv)
+    p, w = oracle.build_tree(uv, seq)
+    assert n == len(seq)
+    assert np.array_equal(s_d[:n].cpu().numpy().view(np.uint32), seq)
+    assert np.array_equal(p_d[:n].cpu().numpy().view(np.uint32), p)
+    assert np.array_equal(w_d[:n].cpu().numpy().view(np.uint32), w)
+
+
 @pytest.mark.parametrize("ov", [4, 2])
 def test_graph2tree_dev_sampled_overflow_few_ids(oracle, gpu, options, ov):
     """The sampled regions overflow on an input with at most 256 ids in use: the
