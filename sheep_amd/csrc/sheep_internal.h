@@ -60,7 +60,7 @@ struct Knobs {
                          //   the lockstep loop: 20 unless off)
   int kb_fresh_lo = 50;  // SHEEP_KB_FRESH_LO / _HI: the kb loop's birth window, in hundredths of
   int kb_fresh_hi = 100; //   the mean degree 2E/B below a bucket's end (tree_from_sorted)
-  int ff_groups = 8;     // SHEEP_FF_GROUPS: tile groups of the fused front pass (1..8): group g's
+  int ff_groups = 1;     // SHEEP_FF_GROUPS: tile groups of the fused front pass (1..8): group g's
                          //   tiles write their own subregion of every region, so a subregion's
                          //   runs come from one XCD's blocks and merge in its L2 (round 6)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
