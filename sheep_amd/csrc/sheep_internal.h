@@ -63,6 +63,8 @@ struct Knobs {
   int ff_groups = 1;     // SHEEP_FF_GROUPS: tile groups of the fused front pass (1..8): group g's
                          //   tiles write their own subregion of every region, so a subregion's
                          //   runs come from one XCD's blocks and merge in its L2 (round 6)
+  int kb_rlink = 1;      // SHEEP_KB_RLINK: the refresh makes the zipper's first step of pairs from
+                         //   pre-bucket roots (CAS INVALID -> b), leaving the rest to the zipper
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };

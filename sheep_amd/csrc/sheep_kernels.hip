@@ -3295,6 +3295,9 @@ struct ZState {
 // (only edges that have not yet changed the forest are dropped).  ZF_SPINE: the walk of the
 // current pending edge has reached the spine (checked once per pending edge).
 constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u, ZF_LINKED = 4u;
+// A kept pair (KB_LINKED, g) is finished: k_kb_refresh linked the pre-bucket root g (the
+// zipper skips it, k_kb_union unions g with its parent).  INVALID b: dropped.
+constexpr uint32_t KB_LINKED = 0xFFFFFFFEu;
 
 struct ZCount {
   uint32_t steps = 0, cas = 0, fail = 0;
@@ -3527,7 +3530,7 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
         uint64_t idx = cbase + k;
         uint32_t b, a, fl;
         src.get(idx, b, a, fl);
-        if (b != INV) {
+        if (b < KB_LINKED) {
           zstart(s, a, b, fl);
           active = true;
           if (STATS) { edges++; st0 = c.steps; c.root += a < rec.B0; }
@@ -4226,11 +4229,20 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 // of a without this edge (zip_step would stop it at its first step; here it costs two bitmap
 // reads in a flat stream instead of a lane of the zipper's queue).  A mark this launch has not
 // set yet only keeps a pair.
+// pj (nullable; the one-GPU apply): the zipper's first step for a pair whose start is a
+// pre-bucket root g' (every pair that reaches no giant): g' had no parent before this bucket
+// (so no hint either), and zip_step's first move from it is exactly CAS(parent[g'], INVALID,
+// b).  Done here, in this flat pass with the pair already in registers, instead of through the
+// zipper's lane queue: the pair is then finished — marked KB_LINKED (b = KB_LINKED, a = g'):
+// the zipper skips it and k_kb_union reads it as a linked pre-bucket root.  A CAS that fails
+// leaves the pair to the zipper (another pair linked g' first; parent[g'] == b drops it, as
+// zip_step does).  Zipper insertion is exact under any order of its steps, so running some
+// first steps a kernel early changes nothing.
 __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept,
                              uint32_t* uf, const uint32_t* __restrict__ label, uint32_t* bitmap,
                              uint32_t B0, uint32_t anchor, uint32_t* gbits,
                              const uint32_t* __restrict__ gx, const uint32_t* __restrict__ anc,
-                             int drop2) {
+                             int drop2, uint32_t* pj = nullptr) {
   const uint32_t nk = *n_kept;
   anchor = anchor_rank(anchor, anc);
   const uint32_t RG = anchor != INV ? uf_find_ro(uf, anchor) : INV;
@@ -4256,7 +4268,13 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
       kept[i] = ~0ull;
     } else {
       const uint32_t g2 = label[rt];
-      if (g2 != g) kept[i] = ((uint64_t)b << 32) | g2;
+      uint64_t nv = ((uint64_t)b << 32) | g2;
+      if (pj && b < KB_LINKED) {
+        const uint32_t old = atomicCAS(&pj[2 * (size_t)g2], INV, b);
+        if (old == INV) nv = ((uint64_t)KB_LINKED << 32) | g2;
+        else if (old == b) nv = ~0ull;
+      }
+      if (nv != it) kept[i] = nv;
     }
   }
 }
@@ -4327,9 +4345,20 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
                            uint32_t B1, uint32_t* bitmap,
                            uint32_t anchor, const uint32_t* __restrict__ anc, uint32_t ps,
                            const uint32_t* __restrict__ linked,
-                           const uint32_t* __restrict__ n_linked) {
+                           const uint32_t* __restrict__ n_linked,
+                           const uint64_t* __restrict__ kept = nullptr,
+                           const uint32_t* __restrict__ n_kept = nullptr) {
   anchor = anchor_rank(anchor, anc);
   const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
+  if (kept) {  // the pre-bucket roots k_kb_refresh linked (KB_LINKED pairs)
+    const uint32_t nk = *n_kept;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
+      const uint64_t it = kept[i];
+      if ((uint32_t)(it >> 32) != KB_LINKED) continue;
+      const uint32_t v = (uint32_t)it;
+      uf_union(uf, v, parent[(size_t)ps * v], R);
+    }
+  }
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
   // with the next bucket hold no marks of it yet; the previous bucket cleared its own)
   if (!FOLD)
@@ -4489,6 +4518,8 @@ void launch_gb_rebase(uint32_t* gbits, uint32_t n_seq, const uint32_t* uf, uint3
                      dim3(BLOCK), 0, s, gbits, nwords, uf, anchor, gx_rd, gx_wr);
 }
 
+static bool kb_refresh_links() { return knobs().kb_rlink != 0; }
+
 void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, uint32_t* uf,
                      uint32_t* label, uint32_t* parent, uint32_t* jump, uint64_t* kept,
                      uint32_t* linked, uint32_t* bitmap, uint32_t* spq, uint32_t* counters,
@@ -4505,7 +4536,7 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     if (refresh)
       hipLaunchKernelGGL(k_kb_refresh, dim3(2048), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                          uf, (const uint32_t*)label, bitmap, B0, anchor, gbits, gx, anc,
-                         1);
+                         1, kb_refresh_links() ? parent : (uint32_t*)nullptr);
     if (anchor != INV)  // the spine, and the giant fold of the marked ranks
       hipLaunchKernelGGL((k_kb_spine<true, true>), dim3(grid_for(((uint64_t)(B1 - B0) + 31) / 32 + 1)), dim3(BLOCK),
                          0, s, (const uint32_t*)bitmap, B0, B1, parent, spq, n_spine, scan_limit,
@@ -4530,9 +4561,11 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
   // over (hub buckets: ~500 ranks, ~0.3 M linked roots): a full grid, whatever the width
   unsigned ug = MAX_GRID;
   auto uk = fold ? k_kb_union<true> : k_kb_union<false>;
+  const bool rl = nonempty && refresh && kb_refresh_links();
   hipLaunchKernelGGL(uk, dim3(ug), dim3(BLOCK), 0, s, (const uint32_t*)parent, uf, B0, B1,
                      bitmap, B0 > 0 ? B0 - 1 : INV, anc_next, ps, (const uint32_t*)linked,
-                     (const uint32_t*)n_linked);
+                     (const uint32_t*)n_linked, rl ? (const uint64_t*)kept : (const uint64_t*)nullptr,
+                     rl ? (const uint32_t*)n_kept : (const uint32_t*)nullptr);
   hipLaunchKernelGGL(k_kb_label, dim3(grid_for((uint64_t)(B1 - B0) + 64)), dim3(BLOCK), 0, s,
                      (const uint32_t*)parent, uf, label, B0, B1, counters, bitmap, (int)fold,
                      gbits, gx, ps);

@@ -136,6 +136,8 @@ def test_sequence_from_degrees(oracle, gpu, case):
     (18, 30, 0, {"part_overlap": 3}),  # fused: the degree scatter partitions the records
     (18, 32, 1, {"part_overlap": 3}),  # fused, FILE degrees
     (18, 31, 1, {"part_overlap": 0}),  # the first partition pass in line
+    (18, 33, 0, {"kb_rlink": 0}),   # every kept pair through the zipper's lane queue
+    (18, 34, 1, {"kb_rlink": 0, "kb_pipe": 0}),
 ])
 def test_graph2tree_dev_front_half(oracle, gpu, options, scale, seed, mode, env):
     """The fused device pipeline (sheep_graph2tree_dev) where the rank gathers are partitioned
