@@ -18,6 +18,7 @@
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "sheep_amd kernels are written for gfx950 only"
 #endif
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -59,10 +60,19 @@ static constexpr uint32_t FAULT_STEPS = 1u << 26;
 __device__ __forceinline__ void raise_fault(uint32_t bit) { atomicOr(&g_fault, bit); }
 constexpr uint32_t FAULT_FOREST = 1u, FAULT_UF = 2u, FAULT_KEPT = 4u;
 
+// The address is looked up once per device and cached: hipGetSymbolAddress took ~0.39 ms per
+// call on the GPU host (the 0.39 ms idle gap between check_err's two readbacks at the end of
+// every graph2tree call, profiles/r06/b_rlink_tilemap/*_step_gaps.txt).
 uint32_t* fault_word() {
-  void* p = nullptr;
-  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fault)) != hipSuccess) return nullptr;
-  return (uint32_t*)p;
+  static std::atomic<uint32_t*> cache[64];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+  uint32_t* p = cache[d].load(std::memory_order_acquire);
+  if (p) return p;
+  void* q = nullptr;
+  if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_fault)) != hipSuccess) return nullptr;
+  cache[d].store((uint32_t*)q, std::memory_order_release);
+  return (uint32_t*)q;
 }
 
 static inline unsigned grid_for(uint64_t n, int per_block = BLOCK) {
