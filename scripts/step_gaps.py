@@ -13,13 +13,16 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--first", default="k_front_sample")
     ap.add_argument("--min-us", type=float, default=10.0)
+    ap.add_argument("--prev", action="store_true",
+                    help="the step before the last one, up to the last step's first kernel: its "
+                         "gaps then include the host time between two calls")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if a.first in r["Kernel_Name"]]
     if not starts:
         raise SystemExit(f"no {a.first} in the trace")
-    rows = rows[starts[-1]:]
+    rows = rows[starts[-2]:starts[-1] + 1] if a.prev and len(starts) > 1 else rows[starts[-1]:]
     iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][:48])
           for r in rows]
     t0 = iv[0][0]

@@ -431,7 +431,8 @@ static int part_shift(uint32_t n_rank, uint32_t nd) {  // id >> shift < nd for i
 // ry' = ry, or a sentinel (RY_SELF / RY_OUT / INV) folded into the top of its 32 - XH bits.
 // A buffer of m records holds the u32 array a (4m bytes) then the u16 array b (2m bytes): the
 // second pass writes and the edge pass reads 6 bytes per record instead of 8.  The edge pass
-// restores the digit from the region starts (k_part_cursor) of the position's region.  Only for
+// takes the digit from its tile (k_xd_tile_desc over the region starts of k_part_cursor; the
+// descriptors live in the spare 2 B per record behind the two arrays).  Only for
 // callers where an id >= n_rank fails the call anyway (graph2tree_dev, the multi-rank driver:
 // the degree pass raises ERR_RANGE): such an id loses its high bits here.
 struct P6Ref {
@@ -2658,8 +2659,44 @@ __device__ __forceinline__ void search512_et(const uint32_t* et, const uint32_t*
   for (int k = 0; k < N; ++k) idx[k] = n[k] - 512u;
 }
 
-// IN6 (with PRE): the records are k_part<1>'s packed output; x's digit bits come from the
-// x-digit region starts xst (shx: the digit shift).
+// The edge pass's tile map over k_part<1>'s x-digit regions [xst[d], xst[d + 1]) (exact): tiles
+// of TILE records that never cross a region, so a tile knows its digit and searches nothing
+// (as the second pass's map over the fused pass's regions, k_fs_tile_desc).  Each block scans
+// the ND + 1 starts itself (cheap) and writes the descriptors (first position, digit << 16 |
+// records) of its 256 tile slots; records 0 past the last tile.
+template <uint32_t ND>
+__global__ void __launch_bounds__(ND)
+k_xd_tile_desc(const uint32_t* __restrict__ xst, uint32_t TILE, uint64_t nt, uint2* __restrict__ desc) {
+  static_assert(ND == 256, "one thread per digit");
+  __shared__ uint32_t toff[ND + 1], wsum[ND / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t n = xst[t + 1] - xst[t], c = (n + TILE - 1) / TILE;
+  const uint32_t incl = wave_incl_scan(c);
+  if (lane == 63) wsum[w] = incl;
+  block_sync();
+  uint32_t add = 0, tot = 0;
+  for (int i = 0; i < (int)(ND / 64); ++i) { if (i < w) add += wsum[i]; tot += wsum[i]; }
+  toff[t] = add + incl - c;
+  if (t == 0) toff[ND] = tot;
+  block_sync();
+  const uint64_t j = (uint64_t)blockIdx.x * ND + t;
+  if (j >= nt) return;
+  if (j >= tot) {
+    desc[j] = make_uint2(0u, 0u);
+    return;
+  }
+  uint32_t lo = 0, cnt = ND;  // the last d with toff[d] <= j
+  while (cnt > 0) {
+    const uint32_t h = cnt >> 1;
+    if (toff[lo + h] <= (uint32_t)j) { lo += h + 1; cnt -= h + 1; } else cnt = h;
+  }
+  const uint32_t d = lo - 1, k = (uint32_t)j - toff[d];
+  const uint32_t p0 = xst[d] + k * TILE;
+  desc[j] = make_uint2(p0, (d << 16) | min(TILE, xst[d + 1] - p0));
+}
+
+// IN6 (with PRE): the records are k_part<1>'s packed output; x's digit comes from the tile map
+// (tdesc, k_xd_tile_desc over the x-digit region starts; shx: the digit shift).
 // PK (every rank < 2^26): a staged slot holds bin << 52 | hi << 26 | lo, so the write-out reads
 // its bin instead of searching the tile's run starts for it.
 template <bool PRE, int NT, int IT, bool IN6 = false, bool PK = false>
@@ -2667,17 +2704,26 @@ __global__ void __launch_bounds__(NT)
 k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict__ rank,
            uint32_t n_rank, uint32_t* err, const uint32_t* __restrict__ bins, uint32_t nb,
            unsigned long long* cursor, const unsigned long long* __restrict__ cap_end,
-           uint64_t* __restrict__ out, uint32_t* ovf, const uint32_t* __restrict__ xst, int shx) {
+           uint64_t* __restrict__ out, uint32_t* ovf, const uint2* __restrict__ tdesc, int shx) {
   static_assert(NT >= 512, "one thread per bin in the scan");
   static_assert(!IN6 || PRE, "packed records are second-pass records");
   constexpr int TILE = NT * IT;
   __shared__ uint64_t stage[TILE];
   __shared__ uint32_t hist[512], tstart[512], sb[512], wsum[NT / 64];
   __shared__ unsigned long long gbase[512];
-  __shared__ uint32_t sst[IN6 ? PD_X + 2 : 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
-  const uint32_t tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
+  uint64_t tbase;
+  uint32_t tile_n, tdig = 0;
+  if (IN6) {  // one x-digit region's tile
+    const uint2 dsc = tdesc[blockIdx.x];
+    tbase = dsc.x;
+    tile_n = dsc.y & 0xFFFFu;
+    tdig = dsc.y >> 16;
+    if (tile_n == 0) return;  // (the grid covers the largest tile count)
+  } else {
+    tbase = (uint64_t)blockIdx.x * TILE;
+    tile_n = (uint32_t)min((uint64_t)TILE, m - tbase);
+  }
   if (t < 512) {
     hist[t] = 0;
     const uint32_t i = t ? et_index(t) : 0u;  // Eytzinger order (search512_et; sb[0] unused)
@@ -2696,12 +2742,11 @@ k_edge_bin(const uint2* __restrict__ uv, uint64_t m, const uint32_t* __restrict_
       ea[k] = j < tile_n ? pin.a[tbase + j] : 0u;
       eb[k] = j < tile_n ? pin.b[tbase + j] : (uint16_t)0;
     }
-    tile_regions<PD_X>(xst, tbase, tile_n, sst);  // (the loads above are in flight)
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
       const uint32_t j = (uint32_t)k * NT + t;
       const uint32_t xlo = ((ea[k] & ((1u << xh) - 1u)) << 16) | eb[k];
-      const uint32_t x = (tile_digit(sst, tbase + min(j, tile_n - 1)) << shx) | xlo;
+      const uint32_t x = (tdig << shx) | xlo;
       e[k] = j < tile_n ? make_uint2(x, p6_ry_dec(ea[k] >> xh, xh)) : make_uint2(0, RY_SELF);
     }
   } else {
@@ -2806,15 +2851,23 @@ void launch_edge_bin(const uint32_t* uv, bool pre, uint64_t m, const uint32_t* r
   // 8192-record tiles, 64 KB stage: two blocks of 16 waves per CU (RMAT-26 edge phase: 512 x
   // 16 -> 8.9 ms, 1024 x 16 -> 10.8, 512 x 8 -> 8.5, 1024 x 8 -> 7.8)
   constexpr int NT = 1024, IT = 8;
-  const unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
+  unsigned nt = (unsigned)((m + NT * IT - 1) / (NT * IT));
   const bool in6 = pre && part_ws;
   const bool pk = n_rank <= (1u << 26);  // ranks < n_seq <= n_rank
+  uint2* desc = nullptr;
+  if (in6) {
+    // the tile map over the x-digit regions (round 6: a tile no longer searches its digits),
+    // its descriptors in the spare 2 B per record behind the packed records (uv holds 8 B each)
+    nt += PD_X;  // >= the tiles (one partial tile per region)
+    desc = (uint2*)((char*)uv + 6 * ((m + 3) & ~3ull));
+    hipLaunchKernelGGL(k_xd_tile_desc<PD_X>, dim3((nt + PD_X - 1) / PD_X), dim3(PD_X), 0, s,
+                       (const uint32_t*)(part_ws + PW_XST), (uint32_t)(NT * IT), (uint64_t)nt, desc);
+  }
   auto k = in6 ? (pk ? k_edge_bin<true, NT, IT, true, true> : k_edge_bin<true, NT, IT, true>)
        : pre   ? (pk ? k_edge_bin<true, NT, IT, false, true> : k_edge_bin<true, NT, IT>)
                : (pk ? k_edge_bin<false, NT, IT, false, true> : k_edge_bin<false, NT, IT>);
   hipLaunchKernelGGL(k, dim3(nt), dim3(NT), 0, s, (const uint2*)uv, m, rank, n_rank, err, bins, nb,
-                     cursor, cap_end, out, ovf, in6 ? part_ws + PW_XST : (const uint32_t*)nullptr,
-                     part_shift(n_rank, PD_X));
+                     cursor, cap_end, out, ovf, (const uint2*)desc, part_shift(n_rank, PD_X));
 }
 
 // ---------------------------------------------------------------------------------------
