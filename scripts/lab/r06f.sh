@@ -1,5 +1,5 @@
 # Round 6: the edge pass over a tile map of the x-digit regions (no per-tile digit search):
-# the GPU suite, then bench lines alternating with the library before it (base = HEAD 3d1e
+# the GPU suite, then bench lines alternating with the library before it (base = HEAD 542723d
 # build with the cached walk-guard address), then the inter-call gaps of LJ / RMAT-26.
 export TMPDIR=/tmp
 O=gpurun_out/r06f; mkdir -p $O

@@ -60,9 +60,10 @@ static constexpr uint32_t FAULT_STEPS = 1u << 26;
 __device__ __forceinline__ void raise_fault(uint32_t bit) { atomicOr(&g_fault, bit); }
 constexpr uint32_t FAULT_FOREST = 1u, FAULT_UF = 2u, FAULT_KEPT = 4u;
 
-// The address is looked up once per device and cached: hipGetSymbolAddress took ~0.39 ms per
-// call on the GPU host (the 0.39 ms idle gap between check_err's two readbacks at the end of
-// every graph2tree call, profiles/r06/b_rlink_tilemap/*_step_gaps.txt).
+// The address is looked up once per device and cached (a runtime symbol lookup per
+// synchronising call otherwise).  (Round 6 first took the ~0.3-0.4 ms idle gaps at the end of
+// the traces' last step for this lookup; they are bench.py's own readbacks after its timed
+// loop, and the cache changed no step time: profiles/r06/c_edge_tilemap/.)
 uint32_t* fault_word() {
   static std::atomic<uint32_t*> cache[64];
   int d = 0;
