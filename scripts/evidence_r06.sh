@@ -3,8 +3,8 @@
 # from the same lease's profiles): the GPU suite; the default bench line (both CPU baselines);
 # the LJ / twitter / RMAT-22 (checked) lines; rocprofv3 kernel stats of the headline (4 timed
 # steps + 1 warmup); the PMC passes of one step (FETCH_SIZE, WRITE_SIZE, TCC hit / miss /
-# atomics, LDS, waves: one --pmc run each); the one-rank RCCL driver line; the P = 8 lockstep
-# simulation.  Everything under $OUT.
+# atomics, LDS, waves: one --pmc run each).  Everything under $OUT.  (The one-rank RCCL driver
+# line and the P = 8 lockstep simulation: scripts/evidence_r06_multi.sh, a lease of its own.)
 set -o pipefail
 OUT=${OUT:-gpurun_out/ev_r06}
 mkdir -p "$OUT"
@@ -17,6 +17,4 @@ timeout -k 10 200 python bench.py --workload lj --no-cpu-baseline > "$OUT/bench_
 timeout -k 10 200 python bench.py --workload twitter --no-cpu-baseline > "$OUT/bench_twitter.json" 2>> "$OUT/bench.err" && echo "tw ok" &&
 timeout -k 10 200 python bench.py --scale 22 --seed 22 --no-cpu-baseline --check > "$OUT/bench_rmat22_checked.json" 2>> "$OUT/bench.err" && echo "rmat22 ok" &&
 rm -rf "$OUT/prof" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 4 --warmup 1 --no-cpu-baseline > "$OUT/prof.log" 2>&1 && echo "prof ok" &&
-OUT="$OUT/pmc" PASSES="fetch write tcc lds wave" bash scripts/pmc_r04.sh &&
-timeout -k 10 200 python bench.py --lockstep-1 --no-cpu-baseline --steps 10 --warmup 3 > "$OUT/bench_lockstep1.json" 2>> "$OUT/bench.err" && echo "lockstep-1 ok" &&
-timeout -k 10 400 python scripts/lockstep_sim.py --P 8 --reps 2 > "$OUT/sim.jsonl" 2> "$OUT/sim.err" && echo "sim ok"
+OUT="$OUT/pmc" PASSES="fetch write tcc lds wave" bash scripts/pmc_r04.sh
