@@ -65,6 +65,7 @@ struct Knobs {
                          //   runs come from one XCD's blocks and merge in its L2 (round 6)
   int kb_rlink = 1;      // SHEEP_KB_RLINK: the refresh makes the zipper's first step of pairs from
                          //   pre-bucket roots (CAS INVALID -> b), leaving the rest to the zipper
+  int kb_zgrid = 0;      // SHEEP_KB_ZGRID: blocks of the one-GPU zipper (0: MAX_GRID; lab)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };

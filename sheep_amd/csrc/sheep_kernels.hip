@@ -4613,7 +4613,8 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     // 64 / 256 / 512 / 1024; twitter-shape: 37.7 / 37.6 / 38.9 ms at 64 / 256 / 512; LJ-shape
     // within noise)
     const uint32_t qchunk = 256;
-    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
+    const unsigned zg = knobs().kb_zgrid > 0 ? (unsigned)std::min(knobs().kb_zgrid, MAX_GRID) : MAX_GRID;
+    hipLaunchKernelGGL(zk, dim3(zg), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
                        anchor, scan_limit, qchunk, anc, (const uint32_t*)nullptr);
