@@ -1,3 +1,4 @@
+# (round 6) SHEEP_KB_ZGRID was a lab knob, removed after this run (rejected: DESIGN §9).
 # Round 6 lab: the zipper's grid (SHEEP_KB_ZGRID, lab knob; default 2048 blocks = every chunk of
 # the kept pairs in flight at once).  Hypothesis: the percolation bucket's one long insertion
 # (LJ ~900 steps, 1.15 ms) comes from inserting the bucket's pairs all at once, out of rank

@@ -45,7 +45,7 @@ static const KnobDef kKnobs[] = {
     {"kb_gsum", &Knobs::kb_gsum},         {"eval_pass", &Knobs::eval_pass},
     {"ls_split", &Knobs::ls_split},       {"ls_seq", &Knobs::ls_seq},
     {"kb_merge", &Knobs::kb_merge},       {"ff_groups", &Knobs::ff_groups},
-    {"kb_rlink", &Knobs::kb_rlink},       {"kb_zgrid", &Knobs::kb_zgrid},
+    {"kb_rlink", &Knobs::kb_rlink},
     {"kb_fresh_lo", &Knobs::kb_fresh_lo}, {"kb_fresh_hi", &Knobs::kb_fresh_hi},
 };
 

@@ -65,7 +65,6 @@ struct Knobs {
                          //   runs come from one XCD's blocks and merge in its L2 (round 6)
   int kb_rlink = 1;      // SHEEP_KB_RLINK: the refresh makes the zipper's first step of pairs from
                          //   pre-bucket roots (CAS INVALID -> b), leaving the rest to the zipper
-  int kb_zgrid = 0;      // SHEEP_KB_ZGRID: blocks of the one-GPU zipper (0: MAX_GRID; lab)
   int eval_pass = 31;    // SHEEP_EVAL_PASS: at most 2^eval_pass adjacency entries sorted per pass
                          //   of the partition evaluation (more: passes over id ranges)
 };
@@ -193,9 +192,20 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // m u64 scratch, ws: PART_WS_WORDS u32 scratch); then launch_edge_pass_tiles(pre, ..., pre = true).
 // ws: y / x digit counts, the first pass's u64 cursors, the u32 region starts of both passes'
 // outputs, the second pass's cursors, the first pass's capacity region ends (sheep_kernels.hip).
-// (+ the fused front pass's subregion tables: 8192 u64 starts + 2, cursors, ends, u32 tile map)
-constexpr size_t PART_WS_WORDS =
-    1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024 + 2 * (8192 + 2) + 4 * 8192 + 8192 + 1;
+// The fused front pass's region cursors (k_front_fused: one device-scope atomic per region and
+// tile, ~134 M a call at RMAT-26, performed at the memory side) are spread over memory: cursor
+// q sits at u64 index fs_cix(q) = (q / 8) * SHEEP_FS_CLS + q % 8, eight to a 64-B line and
+// consecutive lines SHEEP_FS_CLS u64 apart (8: contiguous).
+#ifndef SHEEP_FS_CLS
+#define SHEEP_FS_CLS 8
+#endif
+constexpr uint32_t FS_CLS = SHEEP_FS_CLS;
+__host__ __device__ inline uint32_t fs_cix(uint32_t q) { return (q >> 3) * FS_CLS + (q & 7u); }
+constexpr size_t fs_cur_words(uint32_t n) { return 2 * (size_t)((n + 7) / 8) * FS_CLS; }
+// (+ the fused front pass's subregion tables: 8192 u64 starts + 2, cursors (spread), ends, u32
+// tile map)
+constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024 +
+                                 2 * (8192 + 2) + fs_cur_words(8192) + 2 * 8192 + 8192 + 1;
 // p6: the second pass's records are packed to 6 bytes (sheep_kernels.hip "packed 6-byte
 // records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
 bool part_p6_ok(uint32_t n_rank);

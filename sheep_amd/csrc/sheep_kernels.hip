@@ -410,7 +410,8 @@ static_assert(PW_XCUR % 2 == 0 && PW_YCAP % 2 == 0, "u64 arrays");
 // in the second pass's tile map (FS_MAX + 1; k_fs_tile_scan).
 static constexpr uint32_t FF_GMAX = 8, FS_MAX = DEGB_NB * FF_GMAX;
 static constexpr uint32_t PW_FST = PW_YCAP + 2 * PD_Y, PW_FCUR = PW_FST + 2 * (FS_MAX + 2),
-                          PW_FCAP = PW_FCUR + 2 * FS_MAX, PW_FTOFF = PW_FCAP + 2 * FS_MAX;
+                          PW_FCAP = PW_FCUR + (uint32_t)fs_cur_words(FS_MAX),
+                          PW_FTOFF = PW_FCAP + 2 * FS_MAX;
 static_assert(PW_FST % 2 == 0 && PW_FCUR % 2 == 0 && PW_FCAP % 2 == 0, "u64 arrays");
 static_assert(PW_FTOFF + FS_MAX + 1 <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
 // Second-pass records (x, ry): ry's sentinels.
@@ -661,7 +662,7 @@ k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_
              uint64_t mid_slots, unsigned long long* bst, unsigned long long* bcur,
              unsigned long long* bcap, uint32_t* ystart, unsigned long long* ycur,
              unsigned long long* ycap, unsigned long long* ys64 /* nullable: ystart as u64 */,
-             uint32_t G) {
+             uint32_t G, int spread /* cursors at fs_cix(q) (k_front_fused), else at q */) {
   __shared__ unsigned long long ws[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int pass = 0; pass < 2; ++pass) {
@@ -692,11 +693,11 @@ k_front_caps(const uint32_t* __restrict__ scnt, uint32_t NB, uint64_t m, uint64_
         if (pass) {
           if (ystart) ystart[q] = (uint32_t)st;
           if (ys64) ys64[q] = st;
-          ycur[q] = st;
+          ycur[spread ? fs_cix(q) : q] = st;
           ycap[q] = end;
         } else {
           bst[q] = st;
-          bcur[q] = st;
+          bcur[spread ? fs_cix(q) : q] = st;
           bcap[q] = end;
         }
         st = end;
@@ -881,14 +882,14 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
       const uint32_t q = t * G + grp;  // region t's subregion of this tile's group
       uint32_t fit = 0;
       if (c1) {
-        g1 = atomicAdd(&ycur[q], (unsigned long long)c1);
+        g1 = atomicAdd(&ycur[fs_cix(q)], (unsigned long long)c1);
         const unsigned long long cap = ycap[q];
         fit = g1 + c1 <= cap ? c1 : g1 < cap ? (uint32_t)(cap - g1) : 0u;
         if (fit < c1) atomicOr(ovf_y, 1u);
       }
       yfit[t] = fit;
       if (c2) {
-        g2 = atomicAdd(&bcur[q], (unsigned long long)c2);
+        g2 = atomicAdd(&bcur[fs_cix(q)], (unsigned long long)c2);
         if (g2 + c2 > bcap[q]) {
           atomicOr(ovf_x, 1u);
           g2 = ~0ull;
@@ -979,8 +980,8 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
                    : bstart ? bstart[bq + 1]
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
-  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[bq]);  // (a region's fill past its end: dropped)
-  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[bq]);
+  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[fs_cix(bq)]);  // (a region's fill past its end: dropped)
+  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[fs_cix(bq)]);
   if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
     const uint32_t lm = (1u << SH) - 1u;
     for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
@@ -1197,8 +1198,9 @@ __device__ __forceinline__ void hist16s_slices(const unsigned long long* __restr
   if ((uint32_t)t < NB) {
     uint64_t n = 0;
     for (uint32_t q = t * G; q < (t + 1) * G; ++q) {  // the bucket's G subregions
-      n += min(xs[q + 1], xf[q]) - min(xs[q], min(xs[q + 1], xf[q]));
-      n += min(ys[q + 1], yf[q]) - min(ys[q], min(ys[q + 1], yf[q]));
+      const unsigned long long xq = xf[fs_cix(q)], yq = yf[fs_cix(q)];
+      n += min(xs[q + 1], xq) - min(xs[q], min(xs[q + 1], xq));
+      n += min(ys[q + 1], yq) - min(ys[q], min(ys[q + 1], yq));
     }
     ns = (uint32_t)max((uint64_t)1, (n + CH - 1) / CH);
   }
@@ -1238,7 +1240,8 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
   // sequence (vend: its length)
   uint64_t vend = 0;
   for (uint32_t q = b * G; q < (b + 1) * G; ++q)
-    vend += (max(xs[q], min(xs[q + 1], xf[q])) - xs[q]) + (max(ys[q], min(ys[q + 1], yf[q])) - ys[q]);
+    vend += (max(xs[q], min(xs[q + 1], xf[fs_cix(q)])) - xs[q]) +
+            (max(ys[q], min(ys[q + 1], yf[fs_cix(q)])) - ys[q]);
   const uint64_t v0 = (uint64_t)sl * CH, v1 = min(v0 + CH, vend);
   // Rounds of RW = 65528 entries (8191 16-B loads: thread 1023 skips its eighth, so a round
   // counts at most 65528 < 65536 of one id into a u16 half) from the 8-aligned entry below the
@@ -1260,7 +1263,7 @@ k_degb_hist16s(const uint16_t* __restrict__ ex, const unsigned long long* __rest
     const uint32_t bq = b * G + sq % G;
     const unsigned long long* __restrict__ st = sg ? ys : xs;
     const unsigned long long* __restrict__ fl = sg ? yf : xf;
-    const uint64_t z0 = st[bq], len = max(z0, min(st[bq + 1], fl[bq])) - z0;
+    const uint64_t z0 = st[bq], len = max(z0, min(st[bq + 1], fl[fs_cix(bq)])) - z0;
     const uint64_t a = min(max(v0, off), off + len) - off, e = min(max(v1, off), off + len) - off;
     off += len;
     if (a >= e) continue;  // (uniform)
@@ -1443,7 +1446,7 @@ size_t degs_tmp_words(uint64_t m, uint32_t n_ids) {
   // launch_degree_sampled's smaller tables too; the fused pass's x-only entries need at most
   // fs_room(m, FS_MAX) slots, the sampled pass's both endpoints degs_ep_slots
   const uint64_t ep = std::max<uint64_t>(degs_ep_slots(m, NB), fs_room(m, FS_MAX));
-  return 2 * FS_MAX + 2 * 3 * ((size_t)FS_MAX + 1) + (ep + 1) / 2 + 16;
+  return 2 * FS_MAX + 2 * 2 * ((size_t)FS_MAX + 1) + fs_cur_words(FS_MAX) + 2 + (ep + 1) / 2 + 16;
 }
 
 bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode,
@@ -1469,7 +1472,7 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
   hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
                      degs_ep_slots(m, NB), mid_slots, bst, bcur, bcap, part_ws + PW_YST,
                      (unsigned long long*)(part_ws + PW_CUR), (unsigned long long*)(part_ws + PW_YCAP),
-                     (unsigned long long*)nullptr, 1u);
+                     (unsigned long long*)nullptr, 1u, 0);
   if (caps_done) (void)hipEventRecord(caps_done, s);
   const uint32_t nchunks = (uint32_t)((m + DEGB_CHUNK - 1) / DEGB_CHUNK);
   hipLaunchKernelGGL(k_degb_scatter_cap, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
@@ -1529,8 +1532,8 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   if (G > 1 && grid >= G) grid -= grid % G;
   uint32_t* scnt = tmp;
   unsigned long long* bst = (unsigned long long*)(tmp + 2 * FS_MAX);
-  unsigned long long* bcur = bst + FS_MAX + 1;
-  unsigned long long* bcap = bcur + FS_MAX + 1;
+  unsigned long long* bcur = bst + FS_MAX + 1;  // (spread: fs_cix)
+  unsigned long long* bcap = bcur + fs_cur_words(FS_MAX) / 2 + 1;
   uint16_t* ep = (uint16_t*)(((uintptr_t)(bcap + FS_MAX + 1) + 15) & ~(uintptr_t)15);
   unsigned long long* ys64 = (unsigned long long*)(part_ws + PW_FST);
   unsigned long long* ycur = (unsigned long long*)(part_ws + PW_FCUR);
@@ -1546,7 +1549,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                      file_mode, SH, NB, SH, scnt, 1, G, (uint32_t)(FF_NT * FF_IT / FS_STRIDE));
   hipLaunchKernelGGL(k_front_caps, dim3(1), dim3(1024), 0, s, (const uint32_t*)scnt, NB, m,
                      fs_room(m, NB * G), mid_slots, bst, bcur, bcap, (uint32_t*)nullptr, ycur, ycap,
-                     ys64, G);
+                     ys64, G, 1);
   if (mark) mark(mark_arg, "degree_sample");
   uint32_t* oa = (uint32_t*)mid;
   uint16_t* ob = (uint16_t*)(oa + mid_slots);
@@ -2950,7 +2953,7 @@ k_fs_tile_scan(const unsigned long long* __restrict__ st, const unsigned long lo
     const uint32_t q = t * PER + i;
     nt[i] = 0;
     if (q < S) {
-      const unsigned long long f = min(cur[q], cap[q]);
+      const unsigned long long f = min(cur[fs_cix(q)], cap[q]);
       const uint64_t n = f > st[q] ? f - st[q] : 0;
       nt[i] = (uint32_t)((n + TILE - 1) / TILE);
     }
@@ -2986,7 +2989,7 @@ k_fs_tile_desc(const unsigned long long* __restrict__ st, const unsigned long lo
     if (toff[lo + h] <= (uint32_t)j) { lo += h + 1; cnt -= h + 1; } else cnt = h;
   }
   const uint32_t q = lo - 1;
-  const uint64_t k = j - toff[q], p0 = st[q] + k * TILE, f = min(cur[q], cap[q]);
+  const uint64_t k = j - toff[q], p0 = st[q] + k * TILE, f = min(cur[fs_cix(q)], cap[q]);
   const uint32_t n = (uint32_t)min((uint64_t)TILE, f - p0);
   desc[j] = make_uint2((uint32_t)p0, ((q / G) << 16) | n);
 }
@@ -4613,8 +4616,9 @@ void launch_kb_apply(bool nonempty, uint32_t B0, uint32_t B1, uint32_t anchor, u
     // 64 / 256 / 512 / 1024; twitter-shape: 37.7 / 37.6 / 38.9 ms at 64 / 256 / 512; LJ-shape
     // within noise)
     const uint32_t qchunk = 256;
-    const unsigned zg = knobs().kb_zgrid > 0 ? (unsigned)std::min(knobs().kb_zgrid, MAX_GRID) : MAX_GRID;
-    hipLaunchKernelGGL(zk, dim3(zg), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
+    // (a narrower window — 256 or 64 blocks sweeping the pairs in increasing order — made the
+    // percolation bucket's walks longer, not shorter: LJ tree 3.19 -> 3.65 / 6.21 ms)
+    hipLaunchKernelGGL(zk, dim3(MAX_GRID), dim3(BLOCK), 0, s, kept, (const uint32_t*)n_kept,
                        (const uint32_t*)bitmap, (const uint32_t*)spq, (const uint32_t*)n_spine, B0,
                        B1, uf, (const uint32_t*)label, parent, jump, st + 8, linked, n_linked,
                        anchor, scan_limit, qchunk, anc, (const uint32_t*)nullptr);
