@@ -958,7 +958,7 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
             const uint64_t* __restrict__ rec0 = nullptr,
             const unsigned long long* __restrict__ bend = nullptr /* capacity regions' fill */,
             const unsigned long long* __restrict__ bend2 = nullptr /* ... of ep2's regions */,
-            uint32_t G = 1) {
+            uint32_t G = 1, int spread = 0 /* bend / bend2 at fs_cix (k_front_fused's cursors) */) {
   // span words of dynamic LDS (degb_hist_lds): 16 KB for R-MAT-22's 4096-id buckets, where a
   // fixed 128 KB array held the CU to one block
   extern __shared__ uint32_t cnt[];
@@ -980,8 +980,9 @@ k_degb_hist(const uint16_t* __restrict__ ep, const uint32_t* __restrict__ offset
                    : bstart ? bstart[bq + 1]
                             : (b + 1 < NB) ? offsets[(uint64_t)(b + 1) * nchunks]
                                            : (uint64_t)offsets[last] + counts[last];
-  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[fs_cix(bq)]);  // (a region's fill past its end: dropped)
-  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[fs_cix(bq)]);
+  const uint32_t cq = spread ? fs_cix(bq) : bq;
+  if (bend && sg == 0) s1 = min(s1, (uint64_t)bend[cq]);  // (a region's fill past its end: dropped)
+  if (bend2 && sg == 1) s1 = min(s1, (uint64_t)bend2[cq]);
   if (sg == 0 && rec0) {  // the fused front half's records (x, y) of y bucket b: y's id
     const uint32_t lm = (1u << SH) - 1u;
     for (uint64_t i0 = s0; i0 < s1; i0 += 8 * DEGB_THREADS) {
@@ -1576,7 +1577,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                        deg, (const unsigned long long*)bst, stats, DEGB_PLAIN_SMALL,
                        (const uint16_t*)ob, (const unsigned long long*)ys64,
                        (const uint64_t*)nullptr, (const unsigned long long*)bcur,
-                       (const unsigned long long*)ycur, G);
+                       (const unsigned long long*)ycur, G, 1);
   return true;
 }
 
