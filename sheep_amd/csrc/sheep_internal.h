@@ -197,15 +197,21 @@ uint64_t* group_by_bins(const uint32_t* uv, bool pre, uint64_t m, const uint32_t
 // q sits at u64 index fs_cix(q) = (q / 8) * SHEEP_FS_CLS + q % 8, eight to a 64-B line and
 // consecutive lines SHEEP_FS_CLS u64 apart (8: contiguous).
 #ifndef SHEEP_FS_CLS
-#define SHEEP_FS_CLS 8
+#define SHEEP_FS_CLS 64
 #endif
 constexpr uint32_t FS_CLS = SHEEP_FS_CLS;
 __host__ __device__ inline uint32_t fs_cix(uint32_t q) { return (q >> 3) * FS_CLS + (q & 7u); }
 constexpr size_t fs_cur_words(uint32_t n) { return 2 * (size_t)((n + 7) / 8) * FS_CLS; }
 // (+ the fused front pass's subregion tables: 8192 u64 starts + 2, cursors (spread), ends, u32
 // tile map)
+// The second partition pass's x-digit counts (256 u32, added to by every tile of the first pass
+// or the fused pass) are spread the same way: digit i at xh_ix(i) = (i / 16) * XH_CLS + i % 16.
+constexpr uint32_t XH_CLS = 128;
+__host__ __device__ inline uint32_t xh_ix(uint32_t i) { return (i >> 4) * XH_CLS + (i & 15u); }
+constexpr size_t XH_WORDS = (256 / 16) * XH_CLS;
 constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024 +
-                                 2 * (8192 + 2) + fs_cur_words(8192) + 2 * 8192 + 8192 + 1;
+                                 2 * (8192 + 2) + fs_cur_words(8192) + 2 * 8192 + 8192 + 1 +
+                                 1 + XH_WORDS;
 // p6: the second pass's records are packed to 6 bytes (sheep_kernels.hip "packed 6-byte
 // records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
 bool part_p6_ok(uint32_t n_rank);

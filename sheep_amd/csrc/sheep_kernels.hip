@@ -413,7 +413,10 @@ static constexpr uint32_t PW_FST = PW_YCAP + 2 * PD_Y, PW_FCUR = PW_FST + 2 * (F
                           PW_FCAP = PW_FCUR + (uint32_t)fs_cur_words(FS_MAX),
                           PW_FTOFF = PW_FCAP + 2 * FS_MAX;
 static_assert(PW_FST % 2 == 0 && PW_FCUR % 2 == 0 && PW_FCAP % 2 == 0, "u64 arrays");
-static_assert(PW_FTOFF + FS_MAX + 1 <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
+// ...and the x-digit counts, spread (xh_ix, sheep_internal.h): word PW_XH.  (PW_X, the words
+// they used to take, stay unused.)
+static constexpr uint32_t PW_XH = (PW_FTOFF + FS_MAX + 1 + 1) & ~1u;
+static_assert(PW_XH + XH_WORDS <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
 // Second-pass records (x, ry): ry's sentinels.
 constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
 constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
@@ -910,7 +913,7 @@ k_front_fused(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file
     }
   }
   for (uint32_t i = t; i < PD_X; i += FF_NT)
-    if (hxd[i]) atomicAdd(&xhist[i], hxd[i]);
+    if (hxd[i]) atomicAdd(&xhist[xh_ix(i)], hxd[i]);
   block_sync();
 #pragma unroll
   for (int k = 0; k < FF_IT; ++k)
@@ -1495,7 +1498,7 @@ bool launch_degree_sampled(const uint32_t* uv, uint64_t m, uint32_t n_ids, int f
 
 // The fused front pass (k_front_fused) and its histogram: degrees (deg, selfc), the first
 // partition's packed records in mid (mid_slots positions: u32 x array, then u16 y_lo array) and
-// its region tables in part_ws (PW_YST / PW_CUR / PW_YCAP, the x digits at PW_X).  tmp:
+// its region tables in part_ws (PW_FST / PW_FCUR / PW_FCAP, the x digits at PW_XH).  tmp:
 // degs_tmp_words.  ovf_x: an x bucket outgrew its region (the degrees are then incomplete: the
 // caller runs the exact pass); ovf_y: a y region (the histogram's y ids are then incomplete too:
 // the caller runs the exact pass, and partitions again from uv).
@@ -1542,7 +1545,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
   (void)hipMemsetAsync(scnt, 0, 2 * G * DEGB_NB * 4, s);
-  (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
+  (void)hipMemsetAsync(part_ws + PW_XH, 0, XH_WORDS * 4, s);  // the x digits of k_part<1>
   const uint64_t ns = (m + FS_STRIDE - 1) / FS_STRIDE;
   unsigned sg = (unsigned)std::min<uint64_t>((ns + DEGB_THREADS - 1) / DEGB_THREADS, 512);
   sg = (sg + G - 1) / G * G;
@@ -1558,7 +1561,7 @@ bool launch_front_fused(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file
                      (const uint2*)uv, m, n_ids,
                      file_mode, SH, NB, oa, ob, ycur, (const unsigned long long*)ycap, bcur,
                      (const unsigned long long*)bcap, ep, selfc, ovf_y, ovf_x, err,
-                     part_ws + PW_X, part_shift(n_ids, PD_X),
+                     part_ws + PW_XH, part_shift(n_ids, PD_X),
                      (int)(part_shift(n_ids, PD_X) == SH + 2), G);
   if (mark) mark(mark_arg, "front_fused");
   // the x endpoints, then the y ids (the region of y digit b is x bucket b's id range)
@@ -1638,7 +1641,7 @@ k_fh_count(const uint2* __restrict__ uv, uint64_t m, uint32_t n_ids, int file_mo
   }
   block_sync();
   for (uint32_t i = threadIdx.x; i < PD_X; i += blockDim.x)
-    if (xd[i]) atomicAdd(&xdig[i], xd[i]);
+    if (xd[i]) atomicAdd(&xdig[xh_ix(i)], xd[i]);
   for (uint32_t i = threadIdx.x; i < NB; i += blockDim.x) {
     cy[(uint64_t)blockIdx.x * NB + i] = hy[i];
     cx[(uint64_t)blockIdx.x * NB + i] = hx[i];
@@ -1776,10 +1779,10 @@ bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mo
   uint16_t* epx = align16(bx + NB + 2);
   if (selfc) (void)hipMemsetAsync(selfc, 0, (size_t)n_ids * 4, s);
   if (stats) (void)hipMemsetAsync(stats, 0, 12, s);
-  (void)hipMemsetAsync(part_ws + PW_X, 0, PD_X * 4, s);  // the x digits of k_part<1>
+  (void)hipMemsetAsync(part_ws + PW_XH, 0, XH_WORDS * 4, s);  // the x digits of k_part<1>
   const int psh = part_shift(n_ids, PD_X);  // as launch_part_second with n_rank = n_ids
   hipLaunchKernelGGL(k_fh_count, dim3(nchunks), dim3(DEGB_THREADS), 0, s, (const uint2*)uv, m,
-                     n_ids, file_mode, SH, NB, cy, cx, err, psh, part_ws + PW_X);
+                     n_ids, file_mode, SH, NB, cy, cx, err, psh, part_ws + PW_XH);
   tm_offsets(cy, oy, nchunks, NB, NB, gy, by, s);
   tm_offsets(cx, ox, nchunks, NB, NB, gx, bx, s);
   if (mark) mark(mark_arg, "degree_count");
@@ -2914,11 +2917,12 @@ k_part_count(const uint2* __restrict__ uv, uint64_t m, int sh, uint32_t* __restr
 // cursor[d] = exclusive prefix of hist (one block of ND threads); hist is then cleared.
 // starts (nullable): the same prefix as u32, ND + 1 entries (the last = the total) — the digit
 // regions of this pass's output, which a packed (P6) reader needs to restore the digit bits.
-template <uint32_t ND>
+template <uint32_t ND, bool XH = false /* hist spread as the x-digit counts (xh_ix) */>
 __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32_t* starts) {
   __shared__ unsigned long long s[ND + 1];
   uint32_t t = threadIdx.x;
-  s[t] = hist[t];
+  const uint32_t ht = XH ? xh_ix(t) : t;
+  s[t] = hist[ht];
   block_sync();
   if (t == 0) {
     unsigned long long run = 0;
@@ -2931,7 +2935,7 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32
     starts[t] = (uint32_t)s[t];
     if (t == 0) starts[ND] = (uint32_t)s[ND];
   }
-  hist[t] = 0;
+  hist[ht] = 0;
 }
 
 // The second pass's tile map over the fused front pass's y subregions (k_front_fused): the
@@ -3183,7 +3187,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
   }
   if (MODE == 0)
     for (uint32_t i = t; i < PD_X; i += NT)
-      if (hx[i]) atomicAdd(&xhist[i], hx[i]);
+      if (hx[i]) atomicAdd(&xhist[xh_ix(i)], hx[i]);
   block_sync();
   if (t * R < (int)ND) {
     uint32_t add = 0;
@@ -3231,12 +3235,11 @@ void launch_part_first(const uint32_t* uv, uint64_t m, uint32_t n_rank, uint64_t
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   uint32_t* yhist = ws;
-  uint32_t* xhist = ws + PW_X;
+  uint32_t* xhist = ws + PW_XH;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_CUR);
-  if (yhist_ready) {  // counted by the degree pass (launch_degree_bucketed)
-    (void)hipMemsetAsync(xhist, 0, PD_X * 4, s);
-  } else {
-    (void)hipMemsetAsync(ws, 0, PW_CUR * 4, s);
+  (void)hipMemsetAsync(xhist, 0, XH_WORDS * 4, s);
+  if (!yhist_ready) {  // (else counted by the degree pass, launch_degree_bucketed)
+    (void)hipMemsetAsync(ws, 0, PD_Y * 4, s);
     hipLaunchKernelGGL(k_part_count, dim3(1024), dim3(PT_THREADS), 0, s, (const uint2*)uv, m, sh, yhist);
   }
   hipLaunchKernelGGL(k_part_cursor<PD_Y>, dim3(1), dim3(PD_Y), 0, s, yhist, cursor, ws + PW_YST);
@@ -3255,11 +3258,11 @@ void launch_part_first_caps(const uint32_t* uv, uint64_t m, uint32_t n_rank, uin
                             uint64_t mid_slots, uint32_t* ws, uint32_t* ovf, hipStream_t s) {
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
-  (void)hipMemsetAsync(ws + PW_X, 0, PD_X * 4, s);
+  (void)hipMemsetAsync(ws + PW_XH, 0, XH_WORDS * 4, s);
   uint64_t nt = (m + PT0_THREADS * PT0_ITEMS - 1) / (PT0_THREADS * PT0_ITEMS);
   hipLaunchKernelGGL((k_part<0, PT0_THREADS, PT0_ITEMS, PD_Y>), dim3((unsigned)nt),
                      dim3(PT0_THREADS), 0, s, (const uint64_t*)uv, m, mid, mid_slots,
-                     (unsigned long long*)(ws + PW_CUR), ws + PW_X, sh, shx, (const uint32_t*)nullptr,
+                     (unsigned long long*)(ws + PW_CUR), ws + PW_XH, sh, shx, (const uint32_t*)nullptr,
                      n_rank, -1, (const uint32_t*)nullptr, 0, (const unsigned long long*)nullptr,
                      (const unsigned long long*)nullptr,
                      (const unsigned long long*)(ws + PW_YCAP), ovf);
@@ -3273,9 +3276,9 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   if (m == 0) return;
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   const int ysh = std::max(sh - 8, 0);
-  uint32_t* xhist = ws + PW_X;
+  uint32_t* xhist = ws + PW_XH;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
-  hipLaunchKernelGGL(k_part_cursor<PD_X>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
+  hipLaunchKernelGGL(k_part_cursor<PD_X, true>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
   constexpr uint32_t TILE = PT1_THREADS * PT1_ITEMS;
   if (caps && in6) {
     // the fused pass's subregions (launch_front_fused: ws's PW_F* tables, G per y digit): the
