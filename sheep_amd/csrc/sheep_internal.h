@@ -116,7 +116,7 @@ bool launch_degree_bucketed(const uint32_t* uv, uint64_t m, uint32_t n_ids, int 
                             uint32_t* stats = nullptr /* [0] max degree, [1] zero-degree ids */);
 // Fused front half (graph2tree_dev): degrees (deg, selfc, stats as launch_degree_bucketed)
 // and the records (x, y) grouped by y bucket into recs (m u64), the x digits of
-// launch_part_second counted into part_ws[1024, 1280) — what launch_part_first produced.  tmp:
+// launch_part_second counted into part_ws (spread, xh_ix) — what launch_part_first produced.  tmp:
 // fh_tmp_words (1: not applicable, n_ids beyond 2^26).  False when not applicable.
 size_t fh_tmp_words(uint64_t m, uint32_t n_ids);
 bool launch_fh_front(const uint32_t* uv, uint64_t m, uint32_t n_ids, int file_mode, uint32_t* deg,

@@ -397,9 +397,9 @@ static constexpr uint32_t DEGB_HALF = 32768;  // ids counted by one hist workgro
 // (by y) cuts the ids into 1024 ranges (256 KB rank slices for the second pass's gathers), the
 // second (by x) into 256 (1 MB slices for the edge pass's: 1024 x digits made the edge pass
 // 8.2 -> 7.7 ms but the second pass 5.6 -> 8.0 ms, its 8K-record tiles then writing 64-B
-// runs).  part_ws layout (PART_WS_WORDS u32): y-digit counts [0, 1024), x-digit counts
-// [1024, 1280), u64 cursors from word 1280.
-static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_X = 1024, PW_CUR = 1280;
+// runs).  part_ws layout (PART_WS_WORDS u32): y-digit counts [0, 1024), (unused to 1280), u64
+// cursors from word 1280; the x-digit counts are spread at PW_XH (below).
+static constexpr uint32_t PD_Y = 1024, PD_X = 256, PW_CUR = 1280;  // (words 1024-1279: unused)
 // ...then the u32 region starts of both passes' outputs, the second pass's u64 cursors (the
 // first pass's stay: they are its regions' fill) and the first pass's capacity region ends.
 static constexpr uint32_t PW_YST = 1280 + 2 * 1024, PW_XST = PW_YST + PD_Y + 1;
@@ -413,8 +413,8 @@ static constexpr uint32_t PW_FST = PW_YCAP + 2 * PD_Y, PW_FCUR = PW_FST + 2 * (F
                           PW_FCAP = PW_FCUR + (uint32_t)fs_cur_words(FS_MAX),
                           PW_FTOFF = PW_FCAP + 2 * FS_MAX;
 static_assert(PW_FST % 2 == 0 && PW_FCUR % 2 == 0 && PW_FCAP % 2 == 0, "u64 arrays");
-// ...and the x-digit counts, spread (xh_ix, sheep_internal.h): word PW_XH.  (PW_X, the words
-// they used to take, stay unused.)
+// ...and the x-digit counts, spread (xh_ix, sheep_internal.h): word PW_XH.  (Words 1024-1279,
+// where they used to be, stay unused.)
 static constexpr uint32_t PW_XH = (PW_FTOFF + FS_MAX + 1 + 1) & ~1u;
 static_assert(PW_XH + XH_WORDS <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
 // Second-pass records (x, ry): ry's sentinels.
@@ -3278,7 +3278,7 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   const int ysh = std::max(sh - 8, 0);
   uint32_t* xhist = ws + PW_XH;
   unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
-  hipLaunchKernelGGL(k_part_cursor<PD_X, true>, dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
+  hipLaunchKernelGGL((k_part_cursor<PD_X, true>), dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
   constexpr uint32_t TILE = PT1_THREADS * PT1_ITEMS;
   if (caps && in6) {
     // the fused pass's subregions (launch_front_fused: ws's PW_F* tables, G per y digit): the
