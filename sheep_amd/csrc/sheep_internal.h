@@ -211,7 +211,7 @@ __host__ __device__ inline uint32_t xh_ix(uint32_t i) { return (i >> 4) * XH_CLS
 constexpr size_t XH_WORDS = (256 / 16) * XH_CLS;
 constexpr size_t PART_WS_WORDS = 1280 + 2 * 1024 + 1025 + 257 + 2 * 256 + 2 * 1024 +
                                  2 * (8192 + 2) + fs_cur_words(8192) + 2 * 8192 + 8192 + 1 +
-                                 1 + XH_WORDS + 2 + fs_cur_words(256);
+                                 1 + XH_WORDS;
 // p6: the second pass's records are packed to 6 bytes (sheep_kernels.hip "packed 6-byte
 // records"; only where part_p6_ok(n_rank) and an id >= n_rank fails the call).
 bool part_p6_ok(uint32_t n_rank);

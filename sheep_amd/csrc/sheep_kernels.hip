@@ -416,15 +416,7 @@ static_assert(PW_FST % 2 == 0 && PW_FCUR % 2 == 0 && PW_FCAP % 2 == 0, "u64 arra
 // ...and the x-digit counts, spread (xh_ix, sheep_internal.h): word PW_XH.  (Words 1024-1279,
 // where they used to be, stay unused.)
 static constexpr uint32_t PW_XH = (PW_FTOFF + FS_MAX + 1 + 1) & ~1u;
-// ...and (SHEEP_XC_SPREAD) the second pass's u64 x-digit cursors, spread as the fused pass's
-// (fs_cix): word PW_XC.
-#ifndef SHEEP_XC_SPREAD
-#define SHEEP_XC_SPREAD 0
-#endif
-static constexpr bool XC_SPREAD = SHEEP_XC_SPREAD != 0;
-static constexpr uint32_t PW_XC = (PW_XH + (uint32_t)XH_WORDS + 1) & ~1u;
-__host__ __device__ inline uint32_t xc_ix(uint32_t d) { return XC_SPREAD ? fs_cix(d) : d; }
-static_assert(PW_XC + fs_cur_words(PD_X) <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
+static_assert(PW_XH + XH_WORDS <= PART_WS_WORDS, "part_ws holds the fused pass's tables");
 // Second-pass records (x, ry): ry's sentinels.
 constexpr uint32_t RY_SELF = 0xFFFFFFFDu;  // the record is a self-loop
 constexpr uint32_t RY_OUT = 0xFFFFFFFEu;   // y >= n_rank (outside the rank table)
@@ -2938,7 +2930,7 @@ __global__ void k_part_cursor(uint32_t* hist, unsigned long long* cursor, uint32
     s[ND] = run;
   }
   block_sync();
-  cursor[XH ? xc_ix(t) : t] = s[t];  // (XH: the second pass's cursors)
+  cursor[t] = s[t];
   if (starts) {
     starts[t] = (uint32_t)s[t];
     if (t == 0) starts[ND] = (uint32_t)s[ND];
@@ -3182,8 +3174,7 @@ k_part(const uint64_t* __restrict__ in, uint64_t m, uint64_t* __restrict__ out, 
       const uint32_t d = t * R + r;
       tstart[d] = run;
       run += c[r];
-      const unsigned long long g =
-          c[r] ? atomicAdd(&cursor[MODE == 1 ? xc_ix(d) : d], (unsigned long long)c[r]) : 0ull;
+      const unsigned long long g = c[r] ? atomicAdd(&cursor[d], (unsigned long long)c[r]) : 0ull;
       if (MODE == 0) {
         // capacity regions: a run past its digit's end keeps the part that fits (no unwritten
         // hole below the region's end, which the second pass reads up to) and flags the pass
@@ -3286,7 +3277,7 @@ void launch_part_second(const uint64_t* mid, uint64_t m, const uint32_t* rank, u
   const int sh = part_shift(n_rank, PD_Y), shx = part_shift(n_rank, PD_X);
   const int ysh = std::max(sh - 8, 0);
   uint32_t* xhist = ws + PW_XH;
-  unsigned long long* cursor = (unsigned long long*)(ws + (XC_SPREAD ? PW_XC : PW_XCUR));
+  unsigned long long* cursor = (unsigned long long*)(ws + PW_XCUR);
   hipLaunchKernelGGL((k_part_cursor<PD_X, true>), dim3(1), dim3(PD_X), 0, s, xhist, cursor, ws + PW_XST);
   constexpr uint32_t TILE = PT1_THREADS * PT1_ITEMS;
   if (caps && in6) {
