@@ -3366,9 +3366,9 @@ struct ZState {
 // (only edges that have not yet changed the forest are dropped).  ZF_SPINE: the walk of the
 // current pending edge has reached the spine (checked once per pending edge).
 constexpr uint32_t ZF_KEEP = 1u, ZF_SPINE = 2u, ZF_LINKED = 4u;
-// A kept pair (KB_LINKED, g) is finished: k_kb_refresh linked the pre-bucket root g (the
-// zipper skips it, k_kb_union unions g with its parent).  INVALID b: dropped.
-constexpr uint32_t KB_LINKED = 0xFFFFFFFEu;
+// A kept pair written as (hi, lo) = (r, b) with r < b is finished: k_kb_refresh linked the
+// pre-bucket root of union-find root r below the bucket rank b (every real pair has its hi end
+// above its lo end: the zipper skips these, k_kb_union unions r with b).  INVALID hi: dropped.
 
 struct ZCount {
   uint32_t steps = 0, cas = 0, fail = 0;
@@ -3601,7 +3601,7 @@ __device__ __forceinline__ void tree_queue_body(EdgeSrc src, uint64_t n,
         uint64_t idx = cbase + k;
         uint32_t b, a, fl;
         src.get(idx, b, a, fl);
-        if (b < KB_LINKED) {
+        if (b != INV && a < b) {  // (INVALID: dropped; a > b: linked by k_kb_refresh)
           zstart(s, a, b, fl);
           active = true;
           if (STATS) { edges++; st0 = c.steps; c.root += a < rec.B0; }
@@ -4304,8 +4304,9 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
 // pre-bucket root g' (every pair that reaches no giant): g' had no parent before this bucket
 // (so no hint either), and zip_step's first move from it is exactly CAS(parent[g'], INVALID,
 // b).  Done here, in this flat pass with the pair already in registers, instead of through the
-// zipper's lane queue: the pair is then finished — marked KB_LINKED (b = KB_LINKED, a = g'):
-// the zipper skips it and k_kb_union reads it as a linked pre-bucket root.  A CAS that fails
+// zipper's lane queue: the pair is then finished — rewritten as (rt, b), rt = the union-find
+// root of g''s component (rt < B0 <= b: hi below lo, which no real pair has): the zipper skips
+// it and k_kb_union unions rt with b straight from it (no parent load, a root to start from).  A CAS that fails
 // leaves the pair to the zipper (another pair linked g' first; parent[g'] == b drops it, as
 // zip_step does).  Zipper insertion is exact under any order of its steps, so running some
 // first steps a kernel early changes nothing.
@@ -4340,9 +4341,9 @@ __global__ void k_kb_refresh(uint64_t* kept, const uint32_t* __restrict__ n_kept
     } else {
       const uint32_t g2 = label[rt];
       uint64_t nv = ((uint64_t)b << 32) | g2;
-      if (pj && b < KB_LINKED) {
+      if (pj && b != INV) {
         const uint32_t old = atomicCAS(&pj[2 * (size_t)g2], INV, b);
-        if (old == INV) nv = ((uint64_t)KB_LINKED << 32) | g2;
+        if (old == INV) nv = ((uint64_t)rt << 32) | b;
         else if (old == b) nv = ~0ull;
       }
       if (nv != it) kept[i] = nv;
@@ -4421,13 +4422,12 @@ __global__ void k_kb_union(const uint32_t* __restrict__ parent, uint32_t* uf, ui
                            const uint32_t* __restrict__ n_kept = nullptr) {
   anchor = anchor_rank(anchor, anc);
   const uint32_t R = anchor != INV ? uf_find_ro(uf, anchor) : INV;
-  if (kept) {  // the pre-bucket roots k_kb_refresh linked (KB_LINKED pairs)
+  if (kept) {  // the pre-bucket roots k_kb_refresh linked: pairs (rt, b) with rt < b
     const uint32_t nk = *n_kept;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
       const uint64_t it = kept[i];
-      if ((uint32_t)(it >> 32) != KB_LINKED) continue;
-      const uint32_t v = (uint32_t)it;
-      uf_union(uf, v, parent[(size_t)ps * v], R);
+      const uint32_t r = (uint32_t)(it >> 32), b = (uint32_t)it;
+      if (r < b) uf_union(uf, r, b, R);
     }
   }
   // the bucket's giant-path marks are consumed: clear them for the next bucket (words shared
