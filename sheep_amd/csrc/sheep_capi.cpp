@@ -693,18 +693,26 @@ static void tree_from_sorted(Ctx& c, const uint64_t* sorted, uint64_t* spare, ui
     size_t slot = 0;
     for (size_t k = 0; k < nbk; ++k) {
       HIP_CHECK(hipStreamWaitEvent(sa, ev_map[k & 1], 0));
-      auto next = [&]() {
+      // side: map k+1 on the maps' stream beside apply k; else (a fresh map, after apply k)
+      // on the applies' stream itself, which runs it right after the apply anyway — two
+      // cross-stream event hops fewer (~20 us each on the GPU timeline, round 6)
+      auto next = [&](bool side) {
         rebase(k + 1);
         slot = k + 1;
+        if (!side) {
+          map_k(k + 1, sa);
+          HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], sa));
+          return;
+        }
         HIP_CHECK(hipEventRecord(ev_reb[k & 1], sa));
         HIP_CHECK(hipStreamWaitEvent(s2, ev_reb[k & 1], 0));
         map_k(k + 1, s2);
         HIP_CHECK(hipEventRecord(ev_map[(k + 1) & 1], s2));
       };
-      if (k + 1 < nbk && !fresh[k + 1]) next();
+      if (k + 1 < nbk && !fresh[k + 1]) next(true);
       apply_k(k, slot, sa);
       if (sweep[k]) launch_gb_sweep(uf, gbits, bk[k + 1].first, gx + (slot & 1), sa);
-      if (k + 1 < nbk && fresh[k + 1]) next();
+      if (k + 1 < nbk && fresh[k + 1]) next(false);
     }
     if (sa != s) {  // s resumes after the last apply
       HIP_CHECK(hipEventRecord(c.kb_ev[4], sa));
