@@ -4256,67 +4256,10 @@ __global__ void k_kb_spine(const uint32_t* __restrict__ bitmap, uint32_t B0, uin
   const uint32_t R = FOLD ? uf_find_ro(uf, anchor_rank(anchor, anc)) : INV;
   const uint32_t X = (FOLD && gbits) ? *gx : INV;
   const bool set_g = FOLD && X != INV && uf_find_ro(uf, X) == R;
-  if (CHAIN && limit == 64) {
-    // The searches for the next and the previous marked word as wave ballots (round 6): lane i
-    // holds word base + i, so a mark within the wave's 64 words is one ballot away, and the
-    // words within 64 beyond them are ONE more load per lane (the window after, for the
-    // forward search; the window before, for the backward one) — where one thread per word
-    // walked up to 64 words each way, a dependent load per word (12-35 us per bucket).
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const uint32_t wstride = gridDim.x * blockDim.x;
-    for (uint32_t base = w0 + blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base <= w1;
-         base += wstride) {  // (wave-uniform)
-      const uint32_t w = base + lane;
-      uint32_t bits = w <= w1 ? word_in(bitmap, w, B0, B1) : 0u;
-      const uint64_t M = __ballot(bits != 0);
-      if (M == 0) continue;
-      // forward: the first marked word after w within 64 words (w + 64 = the next window's
-      // word at this lane's index), INV if none
-      const uint64_t ahead = (lane < 63) ? (M >> (lane + 1)) : 0ull;
-      const bool need_next = bits && ahead == 0 && w < w1;
-      uint32_t nxt = INV;
-      if (__ballot(need_next)) {
-        const uint32_t v = base + 64 + lane;
-        const uint32_t nb = v <= w1 ? word_in(bitmap, v, B0, B1) : 0u;
-        const uint64_t M2 = __ballot(nb != 0);
-        const uint64_t ok = M2 & ((lane < 63) ? (~0ull >> (63 - lane)) : ~0ull);  // indices <= lane
-        const uint32_t j = ok ? (uint32_t)(__ffsll((unsigned long long)ok) - 1) : 0u;
-        const uint32_t nbj = __shfl(nb, (int)j);
-        if (need_next && ok) nxt = ((base + 64 + j) << 5) + __ffs(nbj) - 1;
-      }
-      {
-        const uint32_t j = ahead ? lane + 1 + (uint32_t)(__ffsll((unsigned long long)ahead) - 1) : lane;
-        const uint32_t bj = __shfl(bits, (int)j);
-        if (bits && ahead) nxt = ((base + j) << 5) + __ffs(bj) - 1;
-      }
-      // backward: a marked word before w within 64 words (the window before, at indices >= lane)
-      bool has_pred = (M & lt) != 0;
-      const bool need_prev = bits && !has_pred && w > w0;
-      if (__ballot(need_prev) && base >= 64) {
-        const uint32_t v = base - 64 + lane;
-        const uint32_t pb = (v >= w0) ? word_in(bitmap, v, B0, B1) : 0u;
-        const uint64_t M3 = __ballot(pb != 0);
-        if (need_prev && (M3 >> lane) != 0) has_pred = true;
-      }
-      if (!bits) continue;
-      if (set_g) atomicOr(&gbits[w], bits);
-      uint32_t cur = (w << 5) + __ffs(bits) - 1;
-      const uint32_t first = cur;
-      if (FOLD) uf[cur] = R;
-      bits &= bits - 1;
-      while (bits) {
-        const uint32_t nx = (w << 5) + __ffs(bits) - 1;
-        bits &= bits - 1;
-        parent[(size_t)ps * cur] = nx;
-        if (FOLD) uf[nx] = R;
-        cur = nx;
-      }
-      if (nxt != INV) parent[(size_t)ps * cur] = nxt;
-      if (!has_pred) spq[atomicAdd(n_spine, 1u)] = first;
-    }
-    return;
-  }
+  // (The forward / backward searches below as wave ballots over 64-word windows, one load per
+  // lane per window: RMAT-26 and RMAT-22 trees within noise, LJ tree +0.12 ms — the spine queue
+  // comes out in another order, and the percolation bucket's zipper is sensitive to it;
+  // profiles/r06/h_spine_fresh/)
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
        w += gridDim.x * blockDim.x) {
     uint32_t bits = word_in(bitmap, w, B0, B1);
